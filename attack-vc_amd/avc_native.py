@@ -1,0 +1,221 @@
+"""ctypes binding of libavc (include/avc.h) — the only way this package computes.
+
+There is deliberately no CPU or ATen fallback: if libavc.so is missing, or the
+tensors are not on a ROCm device, every entry point raises.  The reference
+(/root/reference/attack_utils.py, models.py) has no FFI of its own; this is the
+binding INTEGRATION.md shows a maintainer adding to it.
+"""
+import ctypes
+import os
+import threading
+import weakref
+from typing import Dict, Optional, Tuple
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libavc.so")
+MAX_BLOCKS = 16
+
+PREC = {"fp32": 0, "bf16": 1}
+REDUCE = {"independent": 0, "mean": 1}
+
+
+class SECfg(ctypes.Structure):
+    _fields_ = [("c_in", ctypes.c_int32), ("c_h", ctypes.c_int32), ("c_out", ctypes.c_int32),
+                ("kernel_size", ctypes.c_int32), ("bank_size", ctypes.c_int32),
+                ("bank_scale", ctypes.c_int32), ("c_bank", ctypes.c_int32),
+                ("n_conv_blocks", ctypes.c_int32), ("n_dense_blocks", ctypes.c_int32),
+                ("subsample", ctypes.c_int32 * MAX_BLOCKS), ("act", ctypes.c_int32)]
+
+
+class AttackOpts(ctypes.Structure):
+    _fields_ = [("precision", ctypes.c_int32), ("reduction", ctypes.c_int32),
+                ("use_graph", ctypes.c_int32), ("losses", ctypes.c_void_p),
+                ("grad0", ctypes.c_void_p)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+# (name, restype, argtypes) of every symbol include/avc.h declares
+SIGNATURES = [
+    ("avc_se_weight_count", ctypes.c_size_t, [ctypes.POINTER(SECfg)]),
+    ("avc_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(SECfg), ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.POINTER(ctypes.c_void_p)]),
+    ("avc_destroy", None, [ctypes.c_void_p]),
+    ("avc_se_forward", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_emb_attack", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("avc_get_profile", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_double)]),
+    ("avc_profile_kernel_count", ctypes.c_int, [ctypes.c_void_p]),
+    ("avc_profile_kernel", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_double)]),
+    ("avc_last_error", ctypes.c_char_p, []),
+    ("avc_version", ctypes.c_char_p, []),
+]
+
+
+def lib():
+    """Load libavc.so (built in-tree by __graft_entry__.build()); raise if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"libavc.so not found at {LIB_PATH}; build it with "
+                                   "`python -c 'import __graft_entry__ as g; g.build()'`")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, res, args in SIGNATURES:
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise RuntimeError(lib().avc_last_error().decode(errors="replace"))
+
+
+def _require_gpu(*ts: torch.Tensor):
+    for t in ts:
+        if not t.is_cuda:
+            raise RuntimeError("libavc runs on MI355X (ROCm) devices only; got a tensor on " + str(t.device))
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"libavc expects float32 tensors, got {t.dtype}")
+
+
+def se_cfg_struct(cfg: Dict) -> SECfg:
+    s = SECfg()
+    for k in ("c_in", "c_h", "c_out", "kernel_size", "bank_size", "bank_scale", "c_bank",
+              "n_conv_blocks", "n_dense_blocks", "act"):
+        setattr(s, k, int(cfg[k]))
+    sub = list(cfg["subsample"])[: int(cfg["n_conv_blocks"])]
+    if len(sub) > MAX_BLOCKS:
+        raise RuntimeError(f"at most {MAX_BLOCKS} conv blocks supported")
+    for i, v in enumerate(sub):
+        s.subsample[i] = int(v)
+    return s
+
+
+class Context:
+    """One libavc context (packed weights + workspace) per (module, device)."""
+
+    def __init__(self, cfg: Dict, flat_weights: torch.Tensor, device: int):
+        self.cfg = dict(cfg)
+        self._cs = se_cfg_struct(cfg)
+        w = flat_weights.detach().to("cpu", torch.float32).contiguous()
+        need = lib().avc_se_weight_count(ctypes.byref(self._cs))
+        if w.numel() != need:
+            raise RuntimeError(f"weights: got {w.numel()} values, config needs {need}")
+        h = ctypes.c_void_p()
+        _check(lib().avc_create(int(device), ctypes.byref(self._cs), ctypes.c_void_p(w.data_ptr()),
+                                w.numel(), ctypes.byref(h)))
+        self.h = h
+        self.device = device
+        self._lock = threading.Lock()
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.avc_destroy(h)
+            self.h = None
+
+    def se_forward(self, x: torch.Tensor) -> torch.Tensor:
+        _require_gpu(x)
+        x = x.contiguous()
+        B, C, T = x.shape
+        emb = torch.empty(B, self.cfg["c_out"], device=x.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_se_forward(self.h, ctypes.c_void_p(x.data_ptr()), B, T,
+                                        ctypes.c_void_p(emb.data_ptr()), ctypes.c_void_p(stream)))
+        return emb
+
+    def emb_attack(self, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
+                   reduction="independent", use_graph=True, want_losses=False, want_grad0=False):
+        _require_gpu(vc_tgt, adv_tgt, ptb0)
+        vc_tgt, adv_tgt, ptb0 = vc_tgt.contiguous(), adv_tgt.contiguous(), ptb0.contiguous()
+        if vc_tgt.shape != adv_tgt.shape or vc_tgt.shape != ptb0.shape:
+            raise RuntimeError(f"shape mismatch: vc_tgt {tuple(vc_tgt.shape)}, adv_tgt "
+                               f"{tuple(adv_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
+        if vc_tgt.dim() != 3 or vc_tgt.shape[1] != self.cfg["c_in"]:
+            raise RuntimeError(f"expected [B, {self.cfg['c_in']}, T] input, got {tuple(vc_tgt.shape)}")
+        B, C, T = vc_tgt.shape
+        out = torch.empty_like(vc_tgt)
+        losses = torch.empty(n_iters, B, device=vc_tgt.device) if want_losses and n_iters > 0 else None
+        grad0 = torch.empty_like(vc_tgt) if want_grad0 and n_iters > 0 else None
+        o = AttackOpts(PREC[precision], REDUCE[reduction], 1 if use_graph else 0,
+                       losses.data_ptr() if losses is not None else None,
+                       grad0.data_ptr() if grad0 is not None else None)
+        stream = torch.cuda.current_stream(vc_tgt.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_emb_attack(self.h, ctypes.c_void_p(vc_tgt.data_ptr()),
+                                        ctypes.c_void_p(adv_tgt.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()),
+                                        B, T, float(eps), int(n_iters), ctypes.c_void_p(out.data_ptr()),
+                                        ctypes.byref(o), ctypes.c_void_p(stream)))
+        return out, losses, grad0
+
+    # --- profiling (bench.py roofline) ---------------------------------------------
+    def set_profiling(self, on: bool):
+        _check(lib().avc_set_profiling(self.h, 1 if on else 0))
+
+    def profile(self) -> Tuple[float, Dict[str, Tuple[int, float, float]]]:
+        ms, fl = ctypes.c_double(), ctypes.c_double()
+        _check(lib().avc_get_profile(self.h, ctypes.byref(ms), ctypes.byref(fl)))
+        stats = {}
+        for i in range(lib().avc_profile_kernel_count(self.h)):
+            name = ctypes.create_string_buffer(128)
+            n, t, f = ctypes.c_long(), ctypes.c_double(), ctypes.c_double()
+            _check(lib().avc_profile_kernel(self.h, i, name, 128, ctypes.byref(n), ctypes.byref(t),
+                                            ctypes.byref(f)))
+            stats[name.value.decode()] = (n.value, t.value, f.value)
+        return ms.value, stats
+
+
+_ctx_cache: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def flat_weights(se: torch.nn.Module) -> torch.Tensor:
+    """Speaker-encoder parameters in state_dict order (the layout avc_create expects)."""
+    return torch.cat([v.detach().reshape(-1).to("cpu", torch.float32) for v in se.state_dict().values()])
+
+
+def se_config(se: torch.nn.Module) -> Dict:
+    """Hyper-parameters of a SpeakerEncoder module (ours or the reference's, models.py:213-283)."""
+    if hasattr(se, "avc_config"):
+        return se.avc_config()
+    ks = [m.kernel_size[0] for m in se.conv_bank]
+    bank_scale = ks[1] - ks[0] if len(ks) > 1 else ks[0]
+    act = 1 if isinstance(se.act, torch.nn.LeakyReLU) else 0
+    return dict(c_in=se.conv_bank[0].in_channels, c_h=se.c_h, c_out=se.c_out, kernel_size=se.kernel_size,
+                bank_size=ks[-1], bank_scale=bank_scale, c_bank=se.conv_bank[0].out_channels,
+                n_conv_blocks=se.n_conv_blocks, n_dense_blocks=se.n_dense_blocks,
+                subsample=list(se.subsample), act=act)
+
+
+def context_for(se: torch.nn.Module, device: torch.device) -> Context:
+    """Cached libavc context for this speaker encoder's current weights on `device`."""
+    if device.type != "cuda":
+        raise RuntimeError("libavc runs on MI355X (ROCm) devices only; got " + str(device))
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    version = tuple((p.data_ptr(), p._version) for p in se.parameters())
+    per = _ctx_cache.setdefault(se, {})
+    hit = per.get(dev)
+    if hit is not None and hit[0] == version:
+        return hit[1]
+    ctx = Context(se_config(se), flat_weights(se), dev)
+    per[dev] = (version, ctx)
+    return ctx
+
+
+def speaker_encoder_forward(se: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """SpeakerEncoder.forward (models.py:327-343) on the MI355X; no autograd."""
+    _require_gpu(x)
+    return context_for(se, x.device).se_forward(x)

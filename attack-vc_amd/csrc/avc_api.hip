@@ -1,0 +1,948 @@
+// libavc host side: C ABI (include/avc.h), weight packing, per-(B,T) workspace
+// and launch plans, the on-device attack loop (hipGraph replay per iteration),
+// and per-kernel HIP-event profiling for bench.py's roofline.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/avc.h"
+#include "avc_kernels.h"
+
+namespace avc {
+template <int WM, int WN>
+__global__ void conv_gemm_f32(const Problem* __restrict__ probs);
+__global__ void se_head(HeadArgs A);
+__global__ void attack_init(const float* vc, const float* ptb0, float* ptb, float* m, float* v, float* adv,
+                            float eps, size_t n);
+}  // namespace avc
+
+using namespace avc;
+
+static thread_local std::string g_err;
+
+static int fail(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return 1;
+}
+
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                              \
+    } while (0)
+
+static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+static inline int cdiv(int x, int m) { return (x + m - 1) / m; }
+
+namespace {
+
+struct DevBuf {
+    float* p = nullptr;
+    size_t n = 0;
+};
+
+// A conv layer of the SpeakerEncoder as stored by torch: W[co][ci][k], b[co].
+struct HostConv {
+    int co, ci, k;
+    const float* W;
+    const float* b;
+};
+
+enum LaunchKind { L_GEMM22, L_GEMM21, L_GEMM11, L_HEAD, L_INIT };
+
+struct Launch {
+    int kind;
+    dim3 grid, block;
+    size_t shmem = 0;
+    Problem* dprobs = nullptr;   // device problem table (L_GEMM*)
+    int nprob = 0;
+    HeadArgs head{};
+    double flop = 0;             // algorithmic FLOPs of this launch
+    std::string name;
+};
+
+struct Plan {
+    std::vector<Launch> launches;
+    std::vector<Problem*> owned;
+};
+
+struct Workspace {
+    int B = 0, T = 0;
+    std::vector<int> Tl;        // T_0..T_n (per conv block input lengths)
+    DevBuf xin, adv, vc, ptb, m, v, bank, h0, gbank, gxd, g1, ghx, ghy, emb_fwd, org, tgt, grad0;
+    std::vector<DevBuf> a1, a2, hb;   // per block
+    DevBuf losses, table, scal;
+    int iters_cap = 0;
+    int* step = nullptr;
+    Plan fwd, iter;
+    hipGraphExec_t graph = nullptr;
+    bool built = false;
+};
+
+}  // namespace
+
+struct avc_ctx {
+    int device = 0;
+    avc_se_cfg cfg{};
+    int nb = 0;                         // bank kernels
+    std::vector<int> bank_k;
+    // packed weights (device)
+    std::vector<DevBuf> AtF_bank;       // [K][Mpad]
+    DevBuf AtF_in, AtB_in;
+    std::vector<DevBuf> AtF_c1, AtF_c2, AtB_c1, AtB_c2;
+    DevBuf AtB_bank;
+    std::vector<int> kpadB_bank;        // K rows per bank segment in AtB_bank
+    std::vector<DevBuf> bias_bank;
+    DevBuf bias_in;
+    std::vector<DevBuf> bias_c1, bias_c2;
+    DevBuf head_Wp, head_WpT, head_bias;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_user = nullptr, ev_done = nullptr;
+    Workspace ws;
+    bool profiling = false;
+    std::map<std::string, std::pair<double, double>> prof;   // name -> (total ms, total flop)
+    std::map<std::string, long> prof_n;
+    double prof_iter_ms = 0;
+    int prof_iters = 0;
+    std::vector<std::string> prof_names;
+};
+
+static int dalloc(DevBuf& b, size_t n) {
+    if (b.n >= n && b.p) return 0;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    if (n == 0) return 0;
+    HIPCHK(hipMalloc(&b.p, n * sizeof(float)));
+    b.n = n;
+    return 0;
+}
+
+static void dfree(DevBuf& b) {
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+}
+
+static int upload(DevBuf& b, const std::vector<float>& h) {
+    if (dalloc(b, h.size())) return 1;
+    HIPCHK(hipMemcpy(b.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    return 0;
+}
+
+static void pads_of(int k, int& pl, int& pr) {   // models.py:23-27
+    pl = k / 2;
+    pr = (k % 2 == 0) ? k / 2 - 1 : k / 2;
+}
+
+// forward A^T: At[ci*k + j][co] = W[co][ci][j]  (rows padded to KC, cols to Mpad)
+static std::vector<float> pack_fwd(const HostConv& c, int Mpad, int row_base = 0, int Krows = -1,
+                                   std::vector<float>* into = nullptr, int ci_lo = 0, int ci_n = -1) {
+    if (ci_n < 0) ci_n = c.ci;
+    const int K = Krows < 0 ? rup(ci_n * c.k, KC) : Krows;
+    std::vector<float> local;
+    std::vector<float>& At = into ? *into : local;
+    if (!into) At.assign((size_t)K * Mpad, 0.f);
+    for (int co = 0; co < c.co; ++co)
+        for (int ci = 0; ci < ci_n; ++ci)
+            for (int j = 0; j < c.k; ++j)
+                At[(size_t)(row_base + ci * c.k + j) * Mpad + co] = c.W[((size_t)co * c.ci + ci_lo + ci) * c.k + j];
+    return local;
+}
+
+// dgrad A^T: At[co*k + j][ci] = W[co][ci][j]
+static void pack_bwd(const HostConv& c, int Mpad, int row_base, std::vector<float>& At) {
+    for (int co = 0; co < c.co; ++co)
+        for (int ci = 0; ci < c.ci; ++ci)
+            for (int j = 0; j < c.k; ++j)
+                At[(size_t)(row_base + co * c.k + j) * Mpad + ci] = c.W[((size_t)co * c.ci + ci) * c.k + j];
+}
+
+// head fragment packing for v_mfma_f32_16x16x4_f32: A[16mt + (l&15)][4kk + (l>>4)]
+static void pack_head(const float* W, int Mo, int Ki, bool transpose, float* dst) {
+    const int M = transpose ? Ki : Mo, K = transpose ? Mo : Ki;
+    for (int mt = 0; mt < M / 16; ++mt)
+        for (int kk = 0; kk < K / 4; ++kk)
+            for (int l = 0; l < 64; ++l) {
+                const int row = 16 * mt + (l & 15), col = 4 * kk + (l >> 4);
+                const float v = transpose ? W[(size_t)col * Ki + row] : W[(size_t)row * Ki + col];
+                dst[((size_t)mt * (K / 4) + kk) * 64 + l] = v;
+            }
+}
+
+static size_t weight_count(const avc_se_cfg& c) {
+    size_t n = 0;
+    for (int k = c.bank_scale; k <= c.bank_size; k += c.bank_scale)
+        n += (size_t)c.c_bank * c.c_in * k + c.c_bank;
+    const int cin_cat = c.c_bank * (c.bank_size / c.bank_scale) + c.c_in;
+    n += (size_t)c.c_h * cin_cat + c.c_h;
+    n += 2 * (size_t)c.n_conv_blocks * ((size_t)c.c_h * c.c_h * c.kernel_size + c.c_h);
+    n += 2 * (size_t)c.n_dense_blocks * ((size_t)c.c_h * c.c_h + c.c_h);
+    n += (size_t)c.c_out * c.c_h + c.c_out;
+    return n;
+}
+
+extern "C" size_t avc_se_weight_count(const avc_se_cfg* cfg) { return cfg ? weight_count(*cfg) : 0; }
+extern "C" const char* avc_last_error(void) { return g_err.c_str(); }
+extern "C" const char* avc_version(void) { return "libavc 0.1 (gfx950, fp32 MFMA)"; }
+
+static int validate_cfg(const avc_se_cfg& c) {
+    if (c.c_in <= 0 || c.c_h <= 0 || c.c_out <= 0 || c.c_bank <= 0) return fail("bad channel counts");
+    if (c.bank_scale <= 0 || c.bank_size < c.bank_scale) return fail("bad bank_size/bank_scale");
+    if (c.kernel_size <= 0) return fail("bad kernel_size");
+    if (c.n_conv_blocks < 0 || c.n_conv_blocks > AVC_MAX_BLOCKS) return fail("n_conv_blocks out of range");
+    if (c.n_dense_blocks < 0) return fail("bad n_dense_blocks");
+    if (c.c_h % 16 || c.c_out % 16 || c.c_h > 128 || c.c_out > 128)
+        return fail("libavc head kernel needs c_h, c_out multiples of 16 and <= 128 (got %d, %d)", c.c_h, c.c_out);
+    for (int l = 0; l < c.n_conv_blocks; ++l)
+        if (c.subsample[l] < 1) return fail("subsample[%d] < 1", l);
+    if (c.act != 0 && c.act != 1) return fail("act must be 0 (relu) or 1 (lrelu)");
+    const int S = c.c_h > c.c_out ? c.c_h : c.c_out;
+    const size_t lds = (size_t)(2 * c.n_dense_blocks + 5) * S * 16 * sizeof(float);
+    if (lds > 160 * 1024) return fail("n_dense_blocks too large for the fused head (%zu B LDS)", lds);
+    return 0;
+}
+
+extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, size_t n_weights, avc_ctx** out) {
+    if (!cfgp || !w || !out) return fail("avc_create: null argument");
+    const avc_se_cfg& c = *cfgp;
+    if (validate_cfg(c)) return 1;
+    if (n_weights != weight_count(c))
+        return fail("avc_create: got %zu weights, config needs %zu", n_weights, weight_count(c));
+    HIPCHK(hipSetDevice(device));
+    avc_ctx* ctx = new avc_ctx();
+    ctx->device = device;
+    ctx->cfg = c;
+    for (int k = c.bank_scale; k <= c.bank_size; k += c.bank_scale) ctx->bank_k.push_back(k);
+    ctx->nb = (int)ctx->bank_k.size();
+    const int nb = ctx->nb;
+
+    // ---- walk the flat state_dict-ordered weights
+    const float* p = w;
+    std::vector<HostConv> bank(nb);
+    for (int i = 0; i < nb; ++i) {
+        bank[i] = {c.c_bank, c.c_in, ctx->bank_k[i], p, nullptr};
+        p += (size_t)c.c_bank * c.c_in * ctx->bank_k[i];
+        bank[i].b = p;
+        p += c.c_bank;
+    }
+    const int cin_cat = c.c_bank * nb + c.c_in;
+    HostConv inc{c.c_h, cin_cat, 1, p, nullptr};
+    p += (size_t)c.c_h * cin_cat;
+    inc.b = p;
+    p += c.c_h;
+    std::vector<HostConv> c1(c.n_conv_blocks), c2(c.n_conv_blocks);
+    for (int l = 0; l < c.n_conv_blocks; ++l) {
+        c1[l] = {c.c_h, c.c_h, c.kernel_size, p, nullptr};
+        p += (size_t)c.c_h * c.c_h * c.kernel_size;
+        c1[l].b = p;
+        p += c.c_h;
+    }
+    for (int l = 0; l < c.n_conv_blocks; ++l) {
+        c2[l] = {c.c_h, c.c_h, c.kernel_size, p, nullptr};
+        p += (size_t)c.c_h * c.c_h * c.kernel_size;
+        c2[l].b = p;
+        p += c.c_h;
+    }
+    const int nd = c.n_dense_blocks;
+    std::vector<const float*> dW(2 * nd), dB(2 * nd);
+    for (int l = 0; l < nd; ++l) {   // first_dense_layers
+        dW[2 * l] = p;
+        p += (size_t)c.c_h * c.c_h;
+        dB[2 * l] = p;
+        p += c.c_h;
+    }
+    for (int l = 0; l < nd; ++l) {   // second_dense_layers
+        dW[2 * l + 1] = p;
+        p += (size_t)c.c_h * c.c_h;
+        dB[2 * l + 1] = p;
+        p += c.c_h;
+    }
+    const float* oW = p;
+    p += (size_t)c.c_out * c.c_h;
+    const float* oB = p;
+    p += c.c_out;
+
+    int rc = 0;
+    auto up = [&](DevBuf& b, const std::vector<float>& h) { rc |= upload(b, h); };
+    auto upv = [&](DevBuf& b, const float* src, size_t n) { up(b, std::vector<float>(src, src + n)); };
+
+    // ---- forward packs
+    const int MpadB = rup(c.c_bank, 128);
+    ctx->AtF_bank.resize(nb);
+    ctx->bias_bank.resize(nb);
+    for (int i = 0; i < nb; ++i) {
+        up(ctx->AtF_bank[i], pack_fwd(bank[i], MpadB));
+        upv(ctx->bias_bank[i], bank[i].b, c.c_bank);
+    }
+    {
+        const int MpadH = rup(c.c_h, 128);
+        const int k1 = rup(c.c_bank * nb, KC), k2 = rup(c.c_in, KC);
+        std::vector<float> At((size_t)(k1 + k2) * MpadH, 0.f);
+        pack_fwd(inc, MpadH, 0, k1 + k2, &At, 0, c.c_bank * nb);
+        pack_fwd(inc, MpadH, k1, k1 + k2, &At, c.c_bank * nb, c.c_in);
+        up(ctx->AtF_in, At);
+        upv(ctx->bias_in, inc.b, c.c_h);
+        // in_conv dgrad: M = cin_cat rows (ci), K = c_h (co): At[co][ci] = W[co][ci]
+        const int MpadI = rup(cin_cat, 128);
+        std::vector<float> Bt((size_t)rup(c.c_h, KC) * MpadI, 0.f);
+        pack_bwd(inc, MpadI, 0, Bt);
+        up(ctx->AtB_in, Bt);
+    }
+    ctx->AtF_c1.resize(c.n_conv_blocks);
+    ctx->AtF_c2.resize(c.n_conv_blocks);
+    ctx->AtB_c1.resize(c.n_conv_blocks);
+    ctx->AtB_c2.resize(c.n_conv_blocks);
+    ctx->bias_c1.resize(c.n_conv_blocks);
+    ctx->bias_c2.resize(c.n_conv_blocks);
+    for (int l = 0; l < c.n_conv_blocks; ++l) {
+        const int MpadH = rup(c.c_h, 128);
+        up(ctx->AtF_c1[l], pack_fwd(c1[l], MpadH));
+        up(ctx->AtF_c2[l], pack_fwd(c2[l], MpadH));
+        const int Kb = rup(c.c_h * c.kernel_size, KC);
+        std::vector<float> b1((size_t)Kb * MpadH, 0.f), b2((size_t)Kb * MpadH, 0.f);
+        pack_bwd(c1[l], MpadH, 0, b1);
+        pack_bwd(c2[l], MpadH, 0, b2);
+        up(ctx->AtB_c1[l], b1);
+        up(ctx->AtB_c2[l], b2);
+        upv(ctx->bias_c1[l], c1[l].b, c.c_h);
+        upv(ctx->bias_c2[l], c2[l].b, c.c_h);
+    }
+    {   // bank dgrad: one GEMM over all bank kernels, M = c_in
+        const int MpadX = rup(c.c_in, 128);
+        int Ktot = 0;
+        for (int i = 0; i < nb; ++i) {
+            ctx->kpadB_bank.push_back(rup(c.c_bank * ctx->bank_k[i], KC));
+            Ktot += ctx->kpadB_bank.back();
+        }
+        std::vector<float> At((size_t)Ktot * MpadX, 0.f);
+        int row = 0;
+        for (int i = 0; i < nb; ++i) {
+            pack_bwd(bank[i], MpadX, row, At);
+            row += ctx->kpadB_bank[i];
+        }
+        up(ctx->AtB_bank, At);
+    }
+    {   // head
+        const size_t CC = (size_t)c.c_h * c.c_h;
+        const size_t tot = 2 * nd * CC + (size_t)c.c_out * c.c_h;
+        std::vector<float> Wp(tot), WpT(tot), bias;
+        for (int l = 0; l < 2 * nd; ++l) {
+            pack_head(dW[l], c.c_h, c.c_h, false, Wp.data() + l * CC);
+            pack_head(dW[l], c.c_h, c.c_h, true, WpT.data() + l * CC);
+            bias.insert(bias.end(), dB[l], dB[l] + c.c_h);
+        }
+        pack_head(oW, c.c_out, c.c_h, false, Wp.data() + 2 * nd * CC);
+        pack_head(oW, c.c_out, c.c_h, true, WpT.data() + 2 * nd * CC);
+        bias.insert(bias.end(), oB, oB + c.c_out);
+        up(ctx->head_Wp, Wp);
+        up(ctx->head_WpT, WpT);
+        up(ctx->head_bias, bias);
+    }
+    if (rc) {
+        avc_destroy(ctx);
+        return 1;
+    }
+    hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_user, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming);
+    if (e == hipSuccess) {
+        const int S = c.c_h > c.c_out ? c.c_h : c.c_out;
+        const size_t lds = (size_t)(2 * nd + 5) * S * 16 * sizeof(float);
+        e = hipFuncSetAttribute((const void*)se_head, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    if (e != hipSuccess) {
+        avc_destroy(ctx);
+        return fail("avc_create: %s", hipGetErrorString(e));
+    }
+    *out = ctx;
+    return 0;
+}
+
+static void free_plan(Plan& pl) {
+    for (Problem* p : pl.owned) hipFree(p);
+    pl.owned.clear();
+    pl.launches.clear();
+}
+
+static void free_ws(Workspace& ws) {
+    if (ws.graph) hipGraphExecDestroy(ws.graph);
+    ws.graph = nullptr;
+    free_plan(ws.fwd);
+    free_plan(ws.iter);
+    DevBuf* bufs[] = {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.bank, &ws.h0, &ws.gbank, &ws.gxd,
+                      &ws.g1, &ws.ghx, &ws.ghy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal};
+    for (DevBuf* b : bufs) dfree(*b);
+    for (auto& b : ws.a1) dfree(b);
+    for (auto& b : ws.a2) dfree(b);
+    for (auto& b : ws.hb) dfree(b);
+    ws.a1.clear();
+    ws.a2.clear();
+    ws.hb.clear();
+    if (ws.step) hipFree(ws.step);
+    ws.step = nullptr;
+    ws.built = false;
+    ws.B = ws.T = 0;
+    ws.iters_cap = 0;
+}
+
+extern "C" void avc_destroy(avc_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    free_ws(ctx->ws);
+    for (auto* v : {&ctx->AtF_bank, &ctx->AtF_c1, &ctx->AtF_c2, &ctx->AtB_c1, &ctx->AtB_c2, &ctx->bias_bank,
+                    &ctx->bias_c1, &ctx->bias_c2})
+        for (auto& b : *v) dfree(b);
+    for (DevBuf* b : {&ctx->AtF_in, &ctx->AtB_in, &ctx->AtB_bank, &ctx->bias_in, &ctx->head_Wp,
+                      &ctx->head_WpT, &ctx->head_bias})
+        dfree(*b);
+    if (ctx->ev_user) hipEventDestroy(ctx->ev_user);
+    if (ctx->ev_done) hipEventDestroy(ctx->ev_done);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+// ---------------------------------------------------------------------------------
+// planning
+// ---------------------------------------------------------------------------------
+
+static Seg make_seg(const float* src, const float* mask, int k0, int C, int c_off, int src_C, int src_T, int ks,
+                    int stride, int pl, int pr, int mode) {
+    Seg s{};
+    s.src = src;
+    s.mask = mask;
+    s.k0 = k0;
+    s.kpad = rup(C * ks, KC);
+    s.C = C;
+    s.c_off = c_off;
+    s.src_C = src_C;
+    s.src_T = src_T;
+    s.ks = ks;
+    s.stride = stride;
+    s.pl = pl;
+    s.pr = pr;
+    s.mode = mode;
+    return s;
+}
+
+static Problem base_problem(int M, int Mpad, int N, int T_out, const float* At, const float* bias, int act) {
+    Problem p{};
+    p.M = M;
+    p.Mpad = Mpad;
+    p.N = N;
+    p.T_out = T_out;
+    p.At = At;
+    p.bias = bias;
+    p.act = act;
+    return p;
+}
+
+static void add_seg(Problem& p, const Seg& s) {
+    p.seg[p.nseg++] = s;
+    p.K = s.k0 + s.kpad;
+}
+
+// choose the tile so a launch has enough workgroups to fill 256 CUs
+static int pick_tile(const std::vector<Problem>& ps) {
+    auto count = [&](int MT, int NT) {
+        long n = 0;
+        for (auto& p : ps) n += (long)cdiv(p.M, MT) * cdiv(p.N, NT);
+        return n;
+    };
+    if (count(128, 128) >= 1024) return L_GEMM22;
+    if (count(128, 64) >= 768) return L_GEMM21;
+    return L_GEMM11;
+}
+
+static int add_gemm(Plan& pl, std::vector<Problem> ps, double flop, const char* what) {
+    const int kind = pick_tile(ps);
+    const int MT = kind == L_GEMM11 ? 64 : 128;
+    const int NT = kind == L_GEMM22 ? 128 : 64;
+    int gx = 0, gy = 0;
+    for (auto& p : ps) {
+        if (p.K % KC) return fail("internal: K %d not a multiple of %d", p.K, KC);
+        if (p.Mpad % MT) return fail("internal: Mpad %d not a multiple of %d", p.Mpad, MT);
+        gx = std::max(gx, cdiv(p.N, NT));
+        gy = std::max(gy, cdiv(p.M, MT));
+    }
+    Problem* d = nullptr;
+    HIPCHK(hipMalloc(&d, ps.size() * sizeof(Problem)));
+    HIPCHK(hipMemcpy(d, ps.data(), ps.size() * sizeof(Problem), hipMemcpyHostToDevice));
+    pl.owned.push_back(d);
+    Launch L;
+    L.kind = kind;
+    L.grid = dim3(gx, gy, (unsigned)ps.size());
+    L.block = dim3(256);
+    L.dprobs = d;
+    L.nprob = (int)ps.size();
+    L.flop = flop;
+    static const char* names[] = {"conv_gemm_f32<2,2>", "conv_gemm_f32<2,1>", "conv_gemm_f32<1,1>"};
+    L.name = names[kind];
+    (void)what;
+    pl.launches.push_back(L);
+    return 0;
+}
+
+// SpeakerEncoder forward (models.py:327-343) from `x` up to h_N, then the head.
+static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, bool attack) {
+    const avc_se_cfg& c = ctx->cfg;
+    const int B = ws.B, T = ws.T, nb = ctx->nb;
+    const int N0 = B * T;
+    {   // conv bank: nb problems in one launch
+        std::vector<Problem> ps;
+        double flop = 0;
+        for (int i = 0; i < nb; ++i) {
+            const int k = ctx->bank_k[i];
+            int pl_, pr_;
+            pads_of(k, pl_, pr_);
+            Problem p = base_problem(c.c_bank, rup(c.c_bank, 128), N0, T, ctx->AtF_bank[i].p, ctx->bias_bank[i].p,
+                                     c.act);
+            add_seg(p, make_seg(x, nullptr, 0, c.c_in, 0, c.c_in, T, k, 1, pl_, pr_, SEG_FWD));
+            p.epi = EPI_ACT;
+            p.out0 = ws.bank.p;
+            p.out0_C = nb * c.c_bank;
+            p.out0_coff = i * c.c_bank;
+            if (attack && i == 0) p.tick = ws.step;
+            ps.push_back(p);
+            flop += 2.0 * c.c_bank * c.c_in * k * N0;
+        }
+        if (add_gemm(pl, ps, flop, "bank")) return 1;
+    }
+    {   // in_conv_layer over cat(bank, x) (models.py:103,337-338)
+        Problem p = base_problem(c.c_h, rup(c.c_h, 128), N0, T, ctx->AtF_in.p, ctx->bias_in.p, c.act);
+        add_seg(p, make_seg(ws.bank.p, nullptr, 0, nb * c.c_bank, 0, nb * c.c_bank, T, 1, 1, 0, 0, SEG_FWD));
+        add_seg(p, make_seg(x, nullptr, p.K, c.c_in, 0, c.c_in, T, 1, 1, 0, 0, SEG_FWD));
+        p.epi = EPI_ACT;
+        p.out0 = ws.h0.p;
+        p.out0_C = c.c_h;
+        if (add_gemm(pl, {p}, 2.0 * c.c_h * (nb * c.c_bank + c.c_in) * N0, "in_conv")) return 1;
+    }
+    int kpl, kpr;
+    pads_of(c.kernel_size, kpl, kpr);
+    for (int l = 0; l < c.n_conv_blocks; ++l) {
+        const int Ti = ws.Tl[l], To = ws.Tl[l + 1], s = c.subsample[l];
+        const float* hin = l == 0 ? ws.h0.p : ws.hb[l - 1].p;
+        Problem p1 = base_problem(c.c_h, rup(c.c_h, 128), B * Ti, Ti, ctx->AtF_c1[l].p, ctx->bias_c1[l].p, c.act);
+        add_seg(p1, make_seg(hin, nullptr, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, 1, kpl, kpr, SEG_FWD));
+        p1.epi = EPI_ACT;
+        p1.out0 = ws.a1[l].p;
+        p1.out0_C = c.c_h;
+        if (add_gemm(pl, {p1}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * Ti, "conv1")) return 1;
+        Problem p2 = base_problem(c.c_h, rup(c.c_h, 128), B * To, To, ctx->AtF_c2[l].p, ctx->bias_c2[l].p, c.act);
+        add_seg(p2, make_seg(ws.a1[l].p, nullptr, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, s, kpl, kpr, SEG_FWD));
+        p2.epi = EPI_BLOCK;
+        p2.out0 = ws.a2[l].p;
+        p2.out0_C = c.c_h;
+        p2.out1 = ws.hb[l].p;
+        p2.out1_C = c.c_h;
+        p2.aux0 = hin;
+        p2.aux0_C = c.c_h;
+        p2.aux0_T = Ti;
+        p2.pool_s = s;
+        if (add_gemm(pl, {p2}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * To, "conv2")) return 1;
+    }
+    {   // head
+        Launch L;
+        L.kind = L_HEAD;
+        L.grid = dim3(cdiv(B, 16));
+        L.block = dim3(512);
+        const int S = std::max(c.c_h, c.c_out);
+        L.shmem = (size_t)(2 * c.n_dense_blocks + 5) * S * 16 * sizeof(float);
+        HeadArgs& A = L.head;
+        A.hN = c.n_conv_blocks ? ws.hb[c.n_conv_blocks - 1].p : ws.h0.p;
+        A.g_hN = ws.ghx.p;
+        A.Wp = ctx->head_Wp.p;
+        A.WpT = ctx->head_WpT.p;
+        A.bias = ctx->head_bias.p;
+        A.emb_out = ws.emb_fwd.p;
+        A.tgt = ws.tgt.p;
+        A.org = ws.org.p;
+        A.losses = ws.losses.p;
+        A.step = ws.step;
+        A.B = B;
+        A.C = c.c_h;
+        A.TN = ws.Tl[c.n_conv_blocks];
+        A.D = c.c_out;
+        A.n_dense = c.n_dense_blocks;
+        A.act = c.act;
+        A.mode = attack ? 1 : 0;
+        A.scal = ws.scal.p;
+        const double dense = 2.0 * c.c_h * c.c_h * 2 * c.n_dense_blocks + 2.0 * c.c_out * c.c_h;
+        L.flop = dense * B * (attack ? 2 : 1);
+        L.name = "se_head";
+        pl.launches.push_back(L);
+    }
+    return 0;
+}
+
+// Input-gradient of the SpeakerEncoder back to the perturbation + Adam (fused).
+static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
+    const avc_se_cfg& c = ctx->cfg;
+    const int B = ws.B, T = ws.T, nb = ctx->nb;
+    int kpl, kpr;
+    pads_of(c.kernel_size, kpl, kpr);
+    // gh ping-pong: head wrote g(h_N) into ghx
+    DevBuf* gcur = &ws.ghx;
+    DevBuf* gnext = &ws.ghy;
+    const int MpadH = rup(c.c_h, 128);
+    for (int l = c.n_conv_blocks - 1; l >= 0; --l) {
+        const int Ti = ws.Tl[l], To = ws.Tl[l + 1], s = c.subsample[l];
+        // conv2^T: dY = g(h_{l+1}) * act'(a2_l), stride s, then * act'(a1_l)
+        Problem p2 = base_problem(c.c_h, MpadH, B * Ti, Ti, ctx->AtB_c2[l].p, nullptr, c.act);
+        add_seg(p2, make_seg(gcur->p, ws.a2[l].p, 0, c.c_h, 0, c.c_h, To, c.kernel_size, s, kpl, kpr, SEG_BWD));
+        p2.epi = EPI_MASK;
+        p2.out0 = ws.g1.p;
+        p2.out0_C = c.c_h;
+        p2.aux0 = ws.a1[l].p;
+        p2.aux0_C = c.c_h;
+        p2.aux0_T = Ti;
+        if (add_gemm(pl, {p2}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * To, "conv2_dgrad")) return 1;
+        // conv1^T + residual avg-pool^T
+        Problem p1 = base_problem(c.c_h, MpadH, B * Ti, Ti, ctx->AtB_c1[l].p, nullptr, c.act);
+        add_seg(p1, make_seg(ws.g1.p, nullptr, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, 1, kpl, kpr, SEG_BWD));
+        p1.epi = EPI_POOLT;
+        p1.out0 = gnext->p;
+        p1.out0_C = c.c_h;
+        p1.aux0 = gcur->p;
+        p1.aux0_C = c.c_h;
+        p1.aux0_T = To;
+        p1.pool_s = s;
+        if (add_gemm(pl, {p1}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * Ti, "conv1_dgrad")) return 1;
+        std::swap(gcur, gnext);
+    }
+    const int N0 = B * T;
+    const int cin_cat = nb * c.c_bank + c.c_in;
+    {   // in_conv^T: rows = cat channels; dY = g(h0) * act'(h0)
+        Problem p = base_problem(cin_cat, rup(cin_cat, 128), N0, T, ctx->AtB_in.p, nullptr, c.act);
+        add_seg(p, make_seg(gcur->p, ws.h0.p, 0, c.c_h, 0, c.c_h, T, 1, 1, 0, 0, SEG_BWD));
+        p.epi = EPI_INCONV_T;
+        p.split = nb * c.c_bank;
+        p.out0 = ws.gbank.p;
+        p.out0_C = nb * c.c_bank;
+        p.out1 = ws.gxd.p;
+        p.out1_C = c.c_in;
+        p.aux0 = ws.bank.p;
+        p.aux0_C = nb * c.c_bank;
+        p.aux0_T = T;
+        if (add_gemm(pl, {p}, 2.0 * c.c_h * cin_cat * N0, "in_conv_dgrad")) return 1;
+    }
+    {   // conv bank^T over all kernels + x passthrough + tanh' + Adam
+        Problem p = base_problem(c.c_in, rup(c.c_in, 128), N0, T, ctx->AtB_bank.p, nullptr, c.act);
+        double flop = 0;
+        int k0 = 0;
+        for (int i = 0; i < nb; ++i) {
+            const int k = ctx->bank_k[i];
+            int pl_, pr_;
+            pads_of(k, pl_, pr_);
+            add_seg(p, make_seg(ws.gbank.p, nullptr, k0, c.c_bank, i * c.c_bank, nb * c.c_bank, T, k, 1, pl_, pr_,
+                                SEG_BWD));
+            k0 += ctx->kpadB_bank[i];
+            flop += 2.0 * c.c_bank * c.c_in * k * N0;
+        }
+        if (nb > MAX_SEGS) return fail("bank_size/bank_scale > %d kernels not supported", MAX_SEGS);
+        p.epi = EPI_ADAM;
+        p.aux0 = ws.gxd.p;
+        p.step = ws.step;
+        p.scal = ws.scal.p;
+        AdamArgs& A = p.adam;
+        A.ptb = ws.ptb.p;
+        A.m = ws.m.p;
+        A.v = ws.v.p;
+        A.vc = ws.vc.p;
+        A.adv = ws.adv.p;
+        A.table = ws.table.p;
+        A.grad0 = ws.grad0.p;
+        A.b1c = (float)(1.0 - 0.9);
+        A.b2 = 0.999f;
+        A.b2c = (float)(1.0 - 0.999);
+        A.adam_eps = 1e-8f;
+        if (add_gemm(pl, {p}, flop, "bank_dgrad_adam")) return 1;
+    }
+    return 0;
+}
+
+static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
+    Workspace& ws = ctx->ws;
+    const avc_se_cfg& c = ctx->cfg;
+    if (B <= 0) return fail("batch size must be positive (got %d)", B);
+    // lengths through the blocks + reflect-pad validity (torch: pad < input length)
+    std::vector<int> Tl{T};
+    int maxpad = 0;
+    for (int k : ctx->bank_k) {
+        int a, b;
+        pads_of(k, a, b);
+        maxpad = std::max(maxpad, std::max(a, b));
+    }
+    if (T <= maxpad) return fail("T=%d too short for the conv bank reflect padding (%d)", T, maxpad);
+    int kpl, kpr;
+    pads_of(c.kernel_size, kpl, kpr);
+    for (int l = 0; l < c.n_conv_blocks; ++l) {
+        if (Tl.back() <= std::max(kpl, kpr))
+            return fail("T=%d too short: conv block %d input has %d frames (reflect pad %d)", T, l, Tl.back(),
+                        std::max(kpl, kpr));
+        const int s = c.subsample[l];
+        const int To = (Tl.back() + kpl + kpr - c.kernel_size) / s + 1;
+        const int Tp = cdiv(Tl.back(), s);
+        if (To != Tp) return fail("conv/pool length mismatch at block %d (%d vs %d)", l, To, Tp);
+        Tl.push_back(To);
+    }
+    const bool same = ws.built && ws.B == B && ws.T == T;
+    if (same && n_iters <= ws.iters_cap) return 0;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (!same) {
+        free_ws(ws);
+        ws.B = B;
+        ws.T = T;
+        ws.Tl = Tl;
+        const int nb = ctx->nb;
+        const size_t X = (size_t)B * c.c_in * T;
+        int rc = 0;
+        for (DevBuf* b : {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.gxd, &ws.grad0}) rc |= dalloc(*b, X);
+        rc |= dalloc(ws.bank, (size_t)B * nb * c.c_bank * T);
+        rc |= dalloc(ws.gbank, (size_t)B * nb * c.c_bank * T);
+        const size_t H = (size_t)B * c.c_h * T;
+        for (DevBuf* b : {&ws.h0, &ws.g1, &ws.ghx, &ws.ghy}) rc |= dalloc(*b, H);
+        for (DevBuf* b : {&ws.emb_fwd, &ws.org, &ws.tgt}) rc |= dalloc(*b, (size_t)B * c.c_out);
+        ws.a1.resize(c.n_conv_blocks);
+        ws.a2.resize(c.n_conv_blocks);
+        ws.hb.resize(c.n_conv_blocks);
+        for (int l = 0; l < c.n_conv_blocks; ++l) {
+            rc |= dalloc(ws.a1[l], (size_t)B * c.c_h * Tl[l]);
+            rc |= dalloc(ws.a2[l], (size_t)B * c.c_h * Tl[l + 1]);
+            rc |= dalloc(ws.hb[l], (size_t)B * c.c_h * Tl[l + 1]);
+        }
+        HIPCHK(hipMalloc(&ws.step, sizeof(int)));
+        rc |= dalloc(ws.scal, 4);
+        if (rc) return 1;
+    }
+    const int cap = std::max(n_iters, std::max(ws.iters_cap, 1));
+    if (dalloc(ws.losses, (size_t)cap * B)) return 1;
+    if (dalloc(ws.table, (size_t)cap * 2)) return 1;
+    ws.iters_cap = cap;
+    // (re)build plans: pointers may have moved
+    if (ws.graph) hipGraphExecDestroy(ws.graph);
+    ws.graph = nullptr;
+    free_plan(ws.fwd);
+    free_plan(ws.iter);
+    if (plan_forward(ctx, ws, ws.fwd, ws.xin.p, false)) return 1;
+    if (plan_forward(ctx, ws, ws.iter, ws.adv.p, true)) return 1;
+    if (plan_backward(ctx, ws, ws.iter)) return 1;
+    ws.built = true;
+    return 0;
+}
+
+static hipError_t launch_one(const Launch& L, hipStream_t s) {
+    switch (L.kind) {
+    case L_GEMM22:
+        hipLaunchKernelGGL((conv_gemm_f32<2, 2>), L.grid, L.block, 0, s, L.dprobs);
+        break;
+    case L_GEMM21:
+        hipLaunchKernelGGL((conv_gemm_f32<2, 1>), L.grid, L.block, 0, s, L.dprobs);
+        break;
+    case L_GEMM11:
+        hipLaunchKernelGGL((conv_gemm_f32<1, 1>), L.grid, L.block, 0, s, L.dprobs);
+        break;
+    case L_HEAD:
+        hipLaunchKernelGGL(se_head, L.grid, L.block, L.shmem, s, L.head);
+        break;
+    default:
+        break;
+    }
+    return hipGetLastError();
+}
+
+static int run_plan(avc_ctx* ctx, const Plan& pl, bool prof) {
+    for (const Launch& L : pl.launches) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (prof) {
+            HIPCHK(hipEventCreate(&a));
+            HIPCHK(hipEventCreate(&b));
+            HIPCHK(hipEventRecord(a, ctx->stream));
+        }
+        hipError_t e = launch_one(L, ctx->stream);
+        if (e != hipSuccess) return fail("launch %s: %s", L.name.c_str(), hipGetErrorString(e));
+        if (prof) {
+            HIPCHK(hipEventRecord(b, ctx->stream));
+            HIPCHK(hipEventSynchronize(b));
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, a, b));
+            auto& s = ctx->prof[L.name];
+            s.first += ms;
+            s.second += L.flop;
+            ctx->prof_n[L.name] += 1;
+            hipEventDestroy(a);
+            hipEventDestroy(b);
+        }
+    }
+    return 0;
+}
+
+static int begin_call(avc_ctx* ctx, hipStream_t user) {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipEventRecord(ctx->ev_user, user));
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_user, 0));
+    return 0;
+}
+
+static int end_call(avc_ctx* ctx, hipStream_t user) {
+    HIPCHK(hipEventRecord(ctx->ev_done, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(user, ctx->ev_done, 0));
+    return 0;
+}
+
+extern "C" int avc_se_forward(avc_ctx* ctx, const float* x, int B, int T, float* emb, void* stream) {
+    if (!ctx || !x || !emb) return fail("avc_se_forward: null argument");
+    hipStream_t us = (hipStream_t)stream;
+    if (ensure_ws(ctx, B, T, 1)) return 1;
+    if (begin_call(ctx, us)) return 1;
+    Workspace& ws = ctx->ws;
+    const avc_se_cfg& c = ctx->cfg;
+    HIPCHK(hipMemcpyAsync(ws.xin.p, x, (size_t)B * c.c_in * T * sizeof(float), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    if (run_plan(ctx, ws.fwd, false)) return 1;
+    HIPCHK(hipMemcpyAsync(emb, ws.emb_fwd.p, (size_t)B * c.c_out * sizeof(float), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    return end_call(ctx, us);
+}
+
+extern "C" int avc_set_profiling(avc_ctx* ctx, int enable) {
+    if (!ctx) return fail("null ctx");
+    ctx->profiling = enable != 0;
+    ctx->prof.clear();
+    ctx->prof_n.clear();
+    ctx->prof_iters = 0;
+    return 0;
+}
+
+extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* ptb0, int B,
+                              int T, float eps, int n_iters, float* out_adv, const avc_attack_opts* opts,
+                              void* stream) {
+    if (!ctx || !vc_tgt || !adv_tgt || !ptb0 || !out_adv) return fail("avc_emb_attack: null argument");
+    if (n_iters < 0) return fail("n_iters must be >= 0");
+    avc_attack_opts o{};
+    o.use_graph = 1;
+    if (opts) o = *opts;
+    if (o.precision != AVC_PREC_FP32) return fail("precision %d not available in this build", o.precision);
+    if (o.reduction != AVC_REDUCE_INDEPENDENT && o.reduction != AVC_REDUCE_MEAN)
+        return fail("bad reduction %d", o.reduction);
+    hipStream_t us = (hipStream_t)stream;
+    if (ensure_ws(ctx, B, T, n_iters)) return 1;
+    if (begin_call(ctx, us)) return 1;
+    Workspace& ws = ctx->ws;
+    const avc_se_cfg& c = ctx->cfg;
+    const size_t X = (size_t)B * c.c_in * T;
+    const float gscale = (float)(2.0 / (o.reduction == AVC_REDUCE_MEAN ? (double)B * c.c_out : (double)c.c_out));
+
+    // Adam scalars per step, computed in double like torch's Python-side math
+    std::vector<float> table(2 * (size_t)std::max(n_iters, 1));
+    for (int t = 1; t <= n_iters; ++t) {
+        const double bc1 = 1.0 - std::pow(0.9, t);
+        const double bc2 = 1.0 - std::pow(0.999, t);
+        table[2 * (t - 1)] = (float)(-(1e-3 / bc1));
+        table[2 * (t - 1) + 1] = (float)std::sqrt(bc2);
+    }
+    HIPCHK(hipMemcpyAsync(ws.table.p, table.data(), table.size() * sizeof(float), hipMemcpyHostToDevice,
+                          ctx->stream));
+    const float scal[4] = {eps, gscale, 0.f, 0.f};
+    HIPCHK(hipMemcpyAsync(ws.scal.p, scal, sizeof(scal), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // host staging buffers above are stack/heap locals
+    HIPCHK(hipMemcpyAsync(ws.vc.p, vc_tgt, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    // org_emb = SE(vc_tgt), tgt_emb = SE(adv_tgt)   (attack_utils.py:73-75)
+    HIPCHK(hipMemcpyAsync(ws.xin.p, vc_tgt, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    if (run_plan(ctx, ws.fwd, false)) return 1;
+    HIPCHK(hipMemcpyAsync(ws.org.p, ws.emb_fwd.p, (size_t)B * c.c_out * sizeof(float), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(ws.xin.p, adv_tgt, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    if (run_plan(ctx, ws.fwd, false)) return 1;
+    HIPCHK(hipMemcpyAsync(ws.tgt.p, ws.emb_fwd.p, (size_t)B * c.c_out * sizeof(float), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    // ptb <- ptb0, Adam state 0, adv = vc + eps*tanh(ptb)
+    hipLaunchKernelGGL(attack_init, dim3((unsigned)((X + 255) / 256)), dim3(256), 0, ctx->stream, ws.vc.p, ptb0,
+                       ws.ptb.p, ws.m.p, ws.v.p, ws.adv.p, eps, X);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemsetAsync(ws.step, 0, sizeof(int), ctx->stream));
+
+    if (ctx->profiling) {
+        hipEvent_t a, b;
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+        HIPCHK(hipEventRecord(a, ctx->stream));
+        for (int it = 0; it < n_iters; ++it)
+            if (run_plan(ctx, ws.iter, true)) return 1;
+        HIPCHK(hipEventRecord(b, ctx->stream));
+        HIPCHK(hipEventSynchronize(b));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, a, b));
+        ctx->prof_iter_ms += ms;
+        ctx->prof_iters += n_iters;
+        hipEventDestroy(a);
+        hipEventDestroy(b);
+    } else if (o.use_graph && n_iters > 0) {
+        if (!ws.graph) {
+            hipGraph_t g;
+            HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+            int rc = run_plan(ctx, ws.iter, false);
+            hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+            if (rc) return 1;
+            if (e != hipSuccess) return fail("graph capture: %s", hipGetErrorString(e));
+            e = hipGraphInstantiate(&ws.graph, g, nullptr, nullptr, 0);
+            hipGraphDestroy(g);
+            if (e != hipSuccess) {
+                ws.graph = nullptr;
+                return fail("graph instantiate: %s", hipGetErrorString(e));
+            }
+        }
+        for (int it = 0; it < n_iters; ++it) HIPCHK(hipGraphLaunch(ws.graph, ctx->stream));
+    } else {
+        for (int it = 0; it < n_iters; ++it)
+            if (run_plan(ctx, ws.iter, false)) return 1;
+    }
+    HIPCHK(hipMemcpyAsync(out_adv, ws.adv.p, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    if (o.losses && n_iters > 0)
+        HIPCHK(hipMemcpyAsync(o.losses, ws.losses.p, (size_t)n_iters * B * sizeof(float), hipMemcpyDeviceToDevice,
+                              ctx->stream));
+    if (o.grad0 && n_iters > 0)
+        HIPCHK(hipMemcpyAsync(o.grad0, ws.grad0.p, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    return end_call(ctx, us);
+}
+
+extern "C" int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_flop_per_iter) {
+    if (!ctx) return fail("null ctx");
+    if (ctx->prof_iters == 0) return fail("no profiled iterations");
+    if (ms_per_iter) *ms_per_iter = ctx->prof_iter_ms / ctx->prof_iters;
+    double f = 0;
+    for (auto& kv : ctx->prof) f += kv.second.second;
+    if (gemm_flop_per_iter) *gemm_flop_per_iter = f / ctx->prof_iters;
+    return 0;
+}
+
+extern "C" int avc_profile_kernel_count(avc_ctx* ctx) { return ctx ? (int)ctx->prof.size() : 0; }
+
+extern "C" int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len, long* launches, double* total_ms,
+                                  double* total_flop) {
+    if (!ctx || i < 0 || i >= (int)ctx->prof.size()) return fail("bad profile index");
+    auto it = ctx->prof.begin();
+    std::advance(it, i);
+    if (name && name_len > 0) {
+        strncpy(name, it->first.c_str(), name_len - 1);
+        name[name_len - 1] = 0;
+    }
+    if (launches) *launches = ctx->prof_n[it->first];
+    if (total_ms) *total_ms = it->second.first;
+    if (total_flop) *total_flop = it->second.second;
+    return 0;
+}

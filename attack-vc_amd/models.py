@@ -1,0 +1,122 @@
+"""AdaIN-VC parameter containers with the reference's module tree.
+
+Drop-in for /root/reference/models.py:121-485 as far as the attack path needs:
+  * identical parameter names, shapes and registration order, so a reference
+    ``model.ckpt`` state_dict loads unchanged (data_utils.py:220-221) and
+    ``torch.manual_seed(s); AdaInVC(cfg)`` draws bit-identical default-init
+    weights (pinned by tests/golden/full_T*.npz weight hashes);
+  * ``speaker_encoder(x)`` (models.py:327-343) runs on the MI355X through
+    libavc's HIP kernels (attack-vc_amd/csrc), never through ATen ops.
+
+ContentEncoder / Decoder hold their parameters (for state_dict compatibility
+and the e2e/fb attacks); their HIP forward is not part of this module.
+"""
+from typing import Dict, List
+
+import torch
+import torch.nn as nn
+
+
+def _act_code(act: str) -> int:
+    """models.py:107-118 get_act: "lrelu" -> LeakyReLU(0.01), anything else ReLU."""
+    return 1 if act == "lrelu" else 0
+
+
+class ContentEncoder(nn.Module):
+    """Parameter tree of models.py:121-179 (same registration order)."""
+
+    def __init__(self, c_in: int, c_h: int, c_out: int, kernel_size: int, bank_size: int,
+                 bank_scale: int, c_bank: int, n_conv_blocks: int, subsample: List[int],
+                 act: str, dropout_rate: float):
+        super().__init__()
+        self.n_conv_blocks = n_conv_blocks
+        self.subsample = subsample
+        self.act_name = act
+        self.conv_bank = nn.ModuleList(
+            [nn.Conv1d(c_in, c_bank, kernel_size=k) for k in range(bank_scale, bank_size + 1, bank_scale)])
+        in_channels = c_bank * (bank_size // bank_scale) + c_in
+        self.in_conv_layer = nn.Conv1d(in_channels, c_h, kernel_size=1)
+        self.first_conv_layers = nn.ModuleList(
+            [nn.Conv1d(c_h, c_h, kernel_size=kernel_size) for _ in range(n_conv_blocks)])
+        self.second_conv_layers = nn.ModuleList(
+            [nn.Conv1d(c_h, c_h, kernel_size=kernel_size, stride=sub)
+             for sub, _ in zip(subsample, range(n_conv_blocks))])
+        self.norm_layer = nn.InstanceNorm1d(c_h, affine=False)
+        self.mean_layer = nn.Conv1d(c_h, c_out, kernel_size=1)
+        self.std_layer = nn.Conv1d(c_h, c_out, kernel_size=1)
+        self.dropout_layer = nn.Dropout(p=dropout_rate)
+
+
+class SpeakerEncoder(nn.Module):
+    """models.py:213-343. forward() dispatches to libavc (HIP)."""
+
+    def __init__(self, c_in: int, c_h: int, c_out: int, kernel_size: int, bank_size: int,
+                 bank_scale: int, c_bank: int, n_conv_blocks: int, n_dense_blocks: int,
+                 subsample: List[int], act: str, dropout_rate: float):
+        super().__init__()
+        self.c_in, self.c_h, self.c_out = c_in, c_h, c_out
+        self.kernel_size = kernel_size
+        self.bank_size, self.bank_scale, self.c_bank = bank_size, bank_scale, c_bank
+        self.n_conv_blocks = n_conv_blocks
+        self.n_dense_blocks = n_dense_blocks
+        self.subsample = list(subsample)
+        self.act_name = act
+        self.dropout_rate = dropout_rate
+        self.conv_bank = nn.ModuleList(
+            [nn.Conv1d(c_in, c_bank, kernel_size=k) for k in range(bank_scale, bank_size + 1, bank_scale)])
+        in_channels = c_bank * (bank_size // bank_scale) + c_in
+        self.in_conv_layer = nn.Conv1d(in_channels, c_h, kernel_size=1)
+        self.first_conv_layers = nn.ModuleList(
+            [nn.Conv1d(c_h, c_h, kernel_size=kernel_size) for _ in range(n_conv_blocks)])
+        self.second_conv_layers = nn.ModuleList(
+            [nn.Conv1d(c_h, c_h, kernel_size=kernel_size, stride=sub)
+             for sub, _ in zip(subsample, range(n_conv_blocks))])
+        self.pooling_layer = nn.AdaptiveAvgPool1d(1)
+        self.first_dense_layers = nn.ModuleList([nn.Linear(c_h, c_h) for _ in range(n_dense_blocks)])
+        self.second_dense_layers = nn.ModuleList([nn.Linear(c_h, c_h) for _ in range(n_dense_blocks)])
+        self.output_layer = nn.Linear(c_h, c_out)
+        self.dropout_layer = nn.Dropout(p=dropout_rate)
+
+    def avc_config(self) -> Dict:
+        return dict(c_in=self.c_in, c_h=self.c_h, c_out=self.c_out, kernel_size=self.kernel_size,
+                    bank_size=self.bank_size, bank_scale=self.bank_scale, c_bank=self.c_bank,
+                    n_conv_blocks=self.n_conv_blocks, n_dense_blocks=self.n_dense_blocks,
+                    subsample=list(self.subsample), act=_act_code(self.act_name))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from avc_native import speaker_encoder_forward
+        return speaker_encoder_forward(self, x)
+
+
+class Decoder(nn.Module):
+    """Parameter tree of models.py:346-401 (sn=False only)."""
+
+    def __init__(self, c_in: int, c_cond: int, c_h: int, c_out: int, kernel_size: int,
+                 n_conv_blocks: int, upsample: List[int], act: str, sn: bool, dropout_rate: float):
+        super().__init__()
+        if sn:
+            raise NotImplementedError("spectral-norm Decoder (sn=True) is not supported by libavc")
+        self.n_conv_blocks = n_conv_blocks
+        self.upsample = upsample
+        self.act_name = act
+        self.in_conv_layer = nn.Conv1d(c_in, c_h, kernel_size=1)
+        self.first_conv_layers = nn.ModuleList(
+            [nn.Conv1d(c_h, c_h, kernel_size=kernel_size) for _ in range(n_conv_blocks)])
+        self.second_conv_layers = nn.ModuleList(
+            [nn.Conv1d(c_h, c_h * up, kernel_size=kernel_size)
+             for _, up in zip(range(n_conv_blocks), self.upsample)])
+        self.norm_layer = nn.InstanceNorm1d(c_h, affine=False)
+        self.conv_affine_layers = nn.ModuleList([nn.Linear(c_cond, c_h * 2) for _ in range(n_conv_blocks * 2)])
+        self.out_conv_layer = nn.Conv1d(c_h, c_out, kernel_size=1)
+        self.dropout_layer = nn.Dropout(p=dropout_rate)
+
+
+class AdaInVC(nn.Module):
+    """models.py:438-452 module tree: content_encoder, speaker_encoder, decoder."""
+
+    def __init__(self, config: Dict):
+        super().__init__()
+        self.config = config
+        self.content_encoder = ContentEncoder(**config["ContentEncoder"])
+        self.speaker_encoder = SpeakerEncoder(**config["SpeakerEncoder"])
+        self.decoder = Decoder(**config["Decoder"])

@@ -1,0 +1,192 @@
+"""Benchmark: defended utterances/s of the AdaIN-VC embedding attack
+(n_iters=1500, eps=0.1) on MI355X — BASELINE.json `metric`, configs[1] workload
+(B=256 utterances of 80x128 normalized mel per GPU).
+
+One "step" = one complete 1500-iteration emb attack over the rank's batch
+(inputs already resident in HBM).  N>1: one process per GPU (torchrun), each
+rank attacks its own contiguous shard of the global batch (no data-path
+collective; scaling "weak"), barrier + max-over-ranks timing.
+
+Also reported:
+  roofline      dominant kernel's algorithmic FLOP / its average launch time
+                (HIP events on libavc's stream, a separate profiled pass after
+                the timed region) vs the gfx950 dense peak for the dtype.
+  cpu_baseline  the reference loop on the host cores (oracle/torch_cpu.py: the
+                reference's own ATen arithmetic, bitwise-pinned), rank 0 at N=1,
+                on a bounded sample scaled to utts/s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "attack-vc_amd"))
+sys.path.insert(0, ROOT)
+
+FULL_CFG = {
+    "SpeakerEncoder": dict(c_in=80, c_h=128, c_out=128, kernel_size=5, bank_size=8, bank_scale=1, c_bank=128,
+                           n_conv_blocks=6, n_dense_blocks=6, subsample=[1, 2, 1, 2, 1, 2], act="relu",
+                           dropout_rate=0.0),
+    "ContentEncoder": dict(c_in=80, c_h=128, c_out=128, kernel_size=5, bank_size=8, bank_scale=1, c_bank=128,
+                           n_conv_blocks=6, subsample=[1, 2, 1, 2, 1, 2], act="relu", dropout_rate=0.0),
+    "Decoder": dict(c_in=128, c_cond=128, c_h=128, c_out=80, kernel_size=5, n_conv_blocks=6,
+                    upsample=[2, 1, 2, 1, 2, 1], act="relu", sn=False, dropout_rate=0.0),
+}
+# emb FLOP per utterance-iteration (SpeakerEncoder fwd + input-grad)
+FLOP_PER_UTT_ITER = 518_848_512
+PEAK = {"fp32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}   # MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=256, help="utterances per GPU")
+    ap.add_argument("--frames", type=int, default=128)
+    ap.add_argument("--n-iters", type=int, default=1500)
+    ap.add_argument("--eps", type=float, default=0.1)
+    ap.add_argument("--precision", default="fp32", choices=["fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(model, budget_s):
+    """Reference emb loop (torch CPU, B=1, all host threads used by ATen)."""
+    from oracle import torch_cpu
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(1)
+    vc, at = torch.randn(1, 80, 128, generator=g), torch.randn(1, 80, 128, generator=g)
+    p0 = torch.randn(1, 80, 128, generator=torch.Generator().manual_seed(123))
+    torch_cpu.emb_attack(sd, FULL_CFG, vc, at, 0.1, 3, p0)            # warm-up
+    stamps = []
+    t0 = time.perf_counter()
+
+    def hook(it):
+        stamps.append(time.perf_counter())
+        if stamps[-1] - t0 > budget_s:
+            raise StopIteration
+
+    try:
+        torch_cpu.emb_attack(sd, FULL_CFG, vc, at, 0.1, 1500, p0, iter_hook=hook)
+    except StopIteration:
+        pass
+    n = len(stamps)
+    per_iter = (stamps[-1] - t0) / n
+    return {"value": 1.0 / (per_iter * 1500), "unit": "utts/s", "cores": threads, "kind": "port",
+            "sample": f"B=1 emb_attack 80x128, {n} of 1500 iterations timed ({per_iter*1e3:.2f} ms/iter), "
+                      f"scaled x1500; oracle/torch_cpu.py (reference ATen arithmetic incl. weight grads)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import attack_utils
+    import avc_native
+    import models
+
+    torch.manual_seed(0)
+    model = models.AdaInVC(FULL_CFG)           # random-init weights of the AdaIN-VC architecture
+    model_dev = model.to(dev)
+    B, T = a.batch, a.frames
+    g = torch.Generator().manual_seed(1)
+    total = B * world
+    vc_all = torch.randn(total, 80, T, generator=g)
+    at_all = torch.randn(total, 80, T, generator=g)
+    p0_all = torch.randn(total, 80, T, generator=torch.Generator().manual_seed(123))
+    sl = slice(rank * B, (rank + 1) * B)
+    vc, at, p0 = (t[sl].contiguous().to(dev) for t in (vc_all, at_all, p0_all))
+    del vc_all, at_all, p0_all
+
+    def step():
+        return attack_utils.emb_attack(model_dev, vc, at, a.eps, a.n_iters, ptb0=p0, precision=a.precision)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out).all()
+
+    roof = None
+    if not a.no_roofline:
+        ctx = avc_native.context_for(model_dev.speaker_encoder, dev)
+        ctx.set_profiling(True)
+        ctx.emb_attack(vc, at, p0, a.eps, 3, precision=a.precision)
+        ms_iter, stats = ctx.profile()
+        ctx.set_profiling(False)
+        name, (n, tot_ms, tot_fl) = max(stats.items(), key=lambda kv: kv[1][1])
+        avg_ms = tot_ms / n
+        achieved = (tot_fl / n) / (avg_ms * 1e-3) / 1e12
+        peak, unit = PEAK[a.precision]
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 4), "traffic": None, "kernel": name,
+                "avg_launch_ms": round(avg_ms, 4), "flop_per_launch": tot_fl / n,
+                "iter_ms_profiled": round(ms_iter, 4),
+                "per_kernel": {k: {"launches_per_iter": v[0] / 3, "avg_ms": round(v[1] / v[0], 4),
+                                   "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 2)} for k, v in stats.items()}}
+        tpath = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tpath):
+            tr = json.load(open(tpath)).get(name)
+            if tr is not None:
+                roof["traffic"] = tr
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(model, a.cpu_seconds)
+
+    if rank == 0:
+        ms = elapsed / a.steps * 1e3
+        value = total * a.steps / elapsed
+        base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+        line = {
+            "metric": base["metric"], "value": round(value, 3), "unit": "utts/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
+            "config": {"workload": f"emb_attack B={B}/GPU T={T} n_iters={a.n_iters} eps={a.eps} "
+                                   f"(BASELINE configs[1]; AdaIN-VC SpeakerEncoder, random init seed 0)",
+                       "batch_per_gpu": B, "frames": T, "n_iters": a.n_iters, "eps": a.eps,
+                       "parallelism": f"dp{world} (independent utterance shards, no collective)"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "flop_per_utt_iter": FLOP_PER_UTT_ITER,
+            "tflops_whole_step": round(FLOP_PER_UTT_ITER * a.n_iters * total * a.steps / elapsed / 1e12, 2),
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

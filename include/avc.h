@@ -1,0 +1,106 @@
+/*
+ * libavc — MI355X (gfx950) adversarial-perturbation engine for AdaIN-VC.
+ *
+ * C ABI: plain pointers and sizes, no torch / HIP C++ types in signatures.
+ * This is the boundary behind the reference's Python attack functions:
+ *
+ *   avc_emb_attack   replaces  attack_utils.emb_attack   (/root/reference/attack_utils.py:51-86)
+ *   avc_se_forward   replaces  SpeakerEncoder.forward    (/root/reference/models.py:327-343)
+ *   avc_create       replaces  AdaInVC(config) + load_state_dict of the speaker encoder
+ *                              (/root/reference/data_utils.py:219-221, models.py:213-283)
+ *
+ * The reference has no native code and no FFI of its own; the Python binding a
+ * maintainer would add is shown in INTEGRATION.md (ctypes).
+ *
+ * Conventions
+ *   - every tensor argument is a DEVICE pointer to contiguous fp32 data in the
+ *     reference's [B, C, T] layout (torch .contiguous() tensors' data_ptr()),
+ *     owned by the caller;  the library owns its workspace (grow-only, per ctx).
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream); all
+ *     work is enqueued on it; calls return after enqueueing (asynchronous).
+ *   - return 0 on success, non-zero on error; avc_last_error() then returns a
+ *     thread-local message.  The Python layer raises RuntimeError(message).
+ *   - one ctx per device; distinct ctx are independent and may be driven from
+ *     different host threads.  A single ctx is not reentrant.
+ */
+#ifndef AVC_H
+#define AVC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVC_MAX_BLOCKS 16
+
+/* SpeakerEncoder hyper-parameters, config.yaml model.SpeakerEncoder
+ * (/root/reference/models.py:218-232).  act: 0 = ReLU, 1 = LeakyReLU(0.01). */
+typedef struct avc_se_cfg {
+    int32_t c_in, c_h, c_out, kernel_size;
+    int32_t bank_size, bank_scale, c_bank;
+    int32_t n_conv_blocks, n_dense_blocks;
+    int32_t subsample[AVC_MAX_BLOCKS];
+    int32_t act;
+} avc_se_cfg;
+
+/* Arithmetic of the per-iteration loop. FP32: exact-f32 MFMA (v_mfma_f32_32x32x2_f32). */
+enum { AVC_PREC_FP32 = 0, AVC_PREC_BF16 = 1 };
+
+/* Loss reduction over a batch of B utterances.
+ *  INDEPENDENT: each utterance is its own attack (loss summed over utterances,
+ *               each an MSE mean over its embedding) == B reference calls at B=1.
+ *  MEAN:        the reference called on a [B,80,T] tensor (MSE mean over B*D). */
+enum { AVC_REDUCE_INDEPENDENT = 0, AVC_REDUCE_MEAN = 1 };
+
+typedef struct avc_ctx avc_ctx;
+
+/* Number of fp32 values avc_create expects in `weights` for this config. */
+size_t avc_se_weight_count(const avc_se_cfg* cfg);
+
+/* Create a context on HIP device `device`.  `weights` is a HOST pointer to the
+ * speaker encoder's parameters concatenated in state_dict order
+ * (conv_bank.{i}.weight, conv_bank.{i}.bias, ..., output_layer.bias), fp32,
+ * `n_weights` == avc_se_weight_count(cfg). */
+int avc_create(int device, const avc_se_cfg* cfg, const float* weights, size_t n_weights,
+               avc_ctx** out);
+
+void avc_destroy(avc_ctx* ctx);
+
+/* emb[B, c_out] = SpeakerEncoder(x[B, c_in, T]) (forward only, fp32). */
+int avc_se_forward(avc_ctx* ctx, const float* x, int B, int T, float* emb, void* stream);
+
+/* Embedding attack (attack_utils.py:51-86) on B utterances of T frames.
+ *   vc_tgt, adv_tgt, ptb0 : [B, c_in, T] device fp32 (ptb0 = the N(0,1) draw of
+ *                           attack_utils.py:68, made by the caller)
+ *   out_adv               : [B, c_in, T] device fp32 = vc_tgt + eps*tanh(ptb)
+ *   losses (optional)     : [n_iters, B] device fp32, per-iteration per-utterance loss
+ *                           L = MSE(emb,tgt) - 0.1*MSE(emb,org) (before that step's update)
+ *   grad0 (optional)      : [B, c_in, T] device fp32, d L / d ptb at iteration 0
+ * Adam(lr=1e-3, betas=(0.9,0.999), eps=1e-8) as torch.optim.Adam defaults. */
+typedef struct avc_attack_opts {
+    int32_t precision;   /* AVC_PREC_* */
+    int32_t reduction;   /* AVC_REDUCE_* */
+    int32_t use_graph;   /* 1 = replay a captured hipGraph per iteration (default) */
+    float* losses;
+    float* grad0;
+} avc_attack_opts;
+
+int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* ptb0,
+                   int B, int T, float eps, int n_iters, float* out_adv,
+                   const avc_attack_opts* opts, void* stream);
+
+/* Average device duration (ms) of the dominant kernel class over the last
+ * avc_emb_attack call on this ctx, measured with HIP events on the ctx's
+ * stream when profiling is enabled via avc_set_profiling(ctx, 1). */
+int avc_set_profiling(avc_ctx* ctx, int enable);
+int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_flop_per_iter);
+
+const char* avc_last_error(void);
+const char* avc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVC_H */

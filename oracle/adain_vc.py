@@ -1,0 +1,350 @@
+"""CPU oracle: numpy restatement of the reference AdaIN-VC attack path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product (attack-vc_amd/) imports,
+links or executes this module; only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg use it, and only as the checker / the timed CPU
+baseline.  It is pinned against golden vectors produced by the real reference
+(tests/golden/make_golden.py -> tests/golden/*.npz; tests/test_oracle_golden.py).
+
+Every function restates the reference's arithmetic, citing the file:line of
+/root/reference it follows.  Activations are [B, C, T] like the reference.
+The backward pass is written out by hand (input-gradient only: the reference
+also accumulates weight gradients it never uses, attack_utils.py:83, SURVEY.md
+8(a) A13; those do not influence the result).
+
+dtype: float32 reproduces the reference's arithmetic type; float64 is used to
+measure fp32 drift.
+"""
+import numpy as np
+from numpy.lib.stride_tricks import sliding_window_view
+
+# ----------------------------------------------------------------------------------
+# primitives
+# ----------------------------------------------------------------------------------
+
+
+def bank_pads(k):
+    """models.py:23-27 (pad_layer): even k -> (k//2, k//2-1), odd k -> (k//2, k//2)."""
+    return (k // 2, k // 2 - 1) if k % 2 == 0 else (k // 2, k // 2)
+
+
+def reflect_pad(x, pl, pr):
+    """models.py:28, F.pad(mode="reflect") (edge sample not repeated)."""
+    if pl == 0 and pr == 0:
+        return x
+    return np.pad(x, ((0, 0), (0, 0), (pl, pr)), mode="reflect")
+
+
+def reflect_pad_backward(gxp, pl, pr, T):
+    """Adjoint of reflect_pad: fold the padded gradient back onto [0,T)."""
+    g = gxp[:, :, pl:pl + T].copy()
+    for i in range(pl):           # padded[i] = x[pl - i]
+        g[:, :, pl - i] += gxp[:, :, i]
+    for i in range(pr):           # padded[pl + T + i] = x[T - 2 - i]
+        g[:, :, T - 2 - i] += gxp[:, :, pl + T + i]
+    return g
+
+
+def conv1d_valid(xp, W, b, stride=1):
+    """nn.Conv1d on an already padded input (models.py:29 layer(inp)).
+    xp [B,Ci,Tp], W [Co,Ci,k], b [Co] -> [B,Co,Tout]."""
+    Co, Ci, k = W.shape
+    win = sliding_window_view(xp, k, axis=2)[:, :, ::stride, :]     # [B,Ci,Tout,k]
+    B, _, Tout, _ = win.shape
+    cols = np.ascontiguousarray(win.transpose(0, 2, 1, 3)).reshape(B, Tout, Ci * k)
+    out = cols @ W.reshape(Co, Ci * k).T                              # [B,Tout,Co]
+    out = out.transpose(0, 2, 1)
+    if b is not None:
+        out = out + b[None, :, None]
+    return np.ascontiguousarray(out)
+
+
+def conv1d_valid_dgrad(gy, W, stride, Tp):
+    """Input gradient of conv1d_valid: gy [B,Co,Tout] -> g_xp [B,Ci,Tp]."""
+    Co, Ci, k = W.shape
+    B, _, Tout = gy.shape
+    gcols = gy.transpose(0, 2, 1) @ W.reshape(Co, Ci * k)             # [B,Tout,Ci*k]
+    gcols = gcols.reshape(B, Tout, Ci, k)
+    gxp = np.zeros((B, Ci, Tp), dtype=gy.dtype)
+    for j in range(k):
+        gxp[:, :, j:j + stride * (Tout - 1) + 1:stride] += gcols[:, :, :, j].transpose(0, 2, 1)
+    return gxp
+
+
+def pad_conv(x, W, b, stride=1):
+    """models.py:10-30 pad_layer: reflect pad by kernel size, then conv."""
+    pl, pr = bank_pads(W.shape[2])
+    return conv1d_valid(reflect_pad(x, pl, pr), W, b, stride)
+
+
+def pad_conv_dgrad(gy, W, stride, T):
+    pl, pr = bank_pads(W.shape[2])
+    gxp = conv1d_valid_dgrad(gy, W, stride, T + pl + pr)
+    return reflect_pad_backward(gxp, pl, pr, T)
+
+
+def relu(x):
+    """models.py:107-118 get_act("relu")."""
+    return np.maximum(x, 0)
+
+
+def avg_pool_ceil(x, s):
+    """F.avg_pool1d(kernel=s, ceil_mode=True) (models.py:206,303): the last
+    window of an odd-length input averages the single remaining sample."""
+    B, C, T = x.shape
+    To = -(-T // s)
+    out = np.zeros((B, C, To), dtype=x.dtype)
+    for t in range(To):
+        lo, hi = s * t, min(s * t + s, T)
+        out[:, :, t] = x[:, :, lo:hi].sum(axis=2) / x.dtype.type(hi - lo)
+    return out
+
+
+def avg_pool_ceil_backward(g, s, T):
+    B, C, To = g.shape
+    gx = np.zeros((B, C, T), dtype=g.dtype)
+    for t in range(To):
+        lo, hi = s * t, min(s * t + s, T)
+        gx[:, :, lo:hi] += (g[:, :, t] / g.dtype.type(hi - lo))[:, :, None]
+    return gx
+
+
+def instance_norm(x, eps=1e-5):
+    """nn.InstanceNorm1d(affine=False) (models.py:176,396): biased variance over T."""
+    mu = x.mean(axis=2, keepdims=True)
+    var = ((x - mu) ** 2).mean(axis=2, keepdims=True)
+    return (x - mu) / np.sqrt(var + x.dtype.type(eps))
+
+
+def linear(x, W, b):
+    """nn.Linear (models.py:276-282, 398)."""
+    return x @ W.T + b
+
+
+# ----------------------------------------------------------------------------------
+# weights
+# ----------------------------------------------------------------------------------
+
+
+class Weights:
+    """state_dict view: w("speaker_encoder.conv_bank.0.weight") -> ndarray."""
+
+    def __init__(self, state, dtype=np.float32):
+        self.d = {k: np.asarray(v, dtype=dtype) for k, v in state.items()}
+
+    def __call__(self, key):
+        return self.d[key]
+
+
+# ----------------------------------------------------------------------------------
+# SpeakerEncoder (models.py:213-343)
+# ----------------------------------------------------------------------------------
+
+
+def se_forward(w, cfg, x, p="speaker_encoder."):
+    """SpeakerEncoder.forward (models.py:327-343). Returns (emb, stash)."""
+    ks = list(range(cfg["bank_scale"], cfg["bank_size"] + 1, cfg["bank_scale"]))
+    st = {"x": x, "bank": []}
+    outs = []
+    for i, k in enumerate(ks):                                         # conv_bank 82-104
+        o = relu(pad_conv(x, w(f"{p}conv_bank.{i}.weight"), w(f"{p}conv_bank.{i}.bias")))
+        outs.append(o)
+    st["bank"] = outs
+    cat = np.concatenate(outs + [x], axis=1)                           # models.py:103
+    h = relu(pad_conv(cat, w(p + "in_conv_layer.weight"), w(p + "in_conv_layer.bias")))  # 337-338
+    st["h0"] = h
+    st["blocks"] = []
+    for l in range(cfg["n_conv_blocks"]):                              # conv_blocks 285-305
+        s = cfg["subsample"][l]
+        a1 = relu(pad_conv(h, w(f"{p}first_conv_layers.{l}.weight"), w(f"{p}first_conv_layers.{l}.bias")))
+        a2 = relu(pad_conv(a1, w(f"{p}second_conv_layers.{l}.weight"),
+                           w(f"{p}second_conv_layers.{l}.bias"), stride=s))
+        res = avg_pool_ceil(h, s) if s > 1 else h
+        st["blocks"].append((h, a1, a2))
+        h = a2 + res
+    st["hN"] = h
+    e = h.mean(axis=2)                                                 # AdaptiveAvgPool1d 275,340
+    st["dense"] = []
+    for l in range(cfg["n_dense_blocks"]):                             # dense_blocks 307-325
+        y1 = relu(linear(e, w(f"{p}first_dense_layers.{l}.weight"), w(f"{p}first_dense_layers.{l}.bias")))
+        y2 = relu(linear(y1, w(f"{p}second_dense_layers.{l}.weight"), w(f"{p}second_dense_layers.{l}.bias")))
+        st["dense"].append((y1, y2))
+        e = y2 + e
+    emb = linear(e, w(p + "output_layer.weight"), w(p + "output_layer.bias"))   # 342
+    return emb, st
+
+
+def se_backward(w, cfg, st, g_emb, p="speaker_encoder."):
+    """Input gradient d(loss)/dx of se_forward given d(loss)/d(emb)."""
+    g = g_emb @ w(p + "output_layer.weight")
+    for l in reversed(range(cfg["n_dense_blocks"])):
+        y1, y2 = st["dense"][l]
+        gy2 = g * (y2 > 0)
+        gy1 = (gy2 @ w(f"{p}second_dense_layers.{l}.weight")) * (y1 > 0)
+        g = g + gy1 @ w(f"{p}first_dense_layers.{l}.weight")
+    T_N = st["hN"].shape[2]
+    gh = np.repeat((g / g.dtype.type(T_N))[:, :, None], T_N, axis=2)
+    for l in reversed(range(cfg["n_conv_blocks"])):
+        s = cfg["subsample"][l]
+        h, a1, a2 = st["blocks"][l]
+        T = h.shape[2]
+        g2 = gh * (a2 > 0)
+        ga1 = pad_conv_dgrad(g2, w(f"{p}second_conv_layers.{l}.weight"), s, T)
+        g1 = ga1 * (a1 > 0)
+        gx = pad_conv_dgrad(g1, w(f"{p}first_conv_layers.{l}.weight"), 1, T)
+        gres = avg_pool_ceil_backward(gh, s, T) if s > 1 else gh
+        gh = gx + gres
+    T = st["x"].shape[2]
+    g0 = gh * (st["h0"] > 0)
+    Wi = w(p + "in_conv_layer.weight")
+    gcat = np.einsum("oc,bot->bct", Wi[:, :, 0], g0)
+    nb = len(st["bank"])
+    cb = st["bank"][0].shape[1]
+    gx = gcat[:, nb * cb:, :].copy()                                   # cat passthrough
+    for i, o in enumerate(st["bank"]):
+        gb = gcat[:, i * cb:(i + 1) * cb, :] * (o > 0)
+        gx += pad_conv_dgrad(gb, w(f"{p}conv_bank.{i}.weight"), 1, T)
+    return gx
+
+
+# ----------------------------------------------------------------------------------
+# ContentEncoder (models.py:121-210) and Decoder (models.py:346-435), forward only
+# ----------------------------------------------------------------------------------
+
+
+def ce_forward(w, cfg, x, p="content_encoder."):
+    """ContentEncoder.forward -> mu (models.py:181-208; log_sigma unused by inference)."""
+    ks = list(range(cfg["bank_scale"], cfg["bank_size"] + 1, cfg["bank_scale"]))
+    outs = [relu(pad_conv(x, w(f"{p}conv_bank.{i}.weight"), w(f"{p}conv_bank.{i}.bias")))
+            for i, _ in enumerate(ks)]
+    out = np.concatenate(outs + [x], axis=1)
+    out = relu(instance_norm(pad_conv(out, w(p + "in_conv_layer.weight"), w(p + "in_conv_layer.bias"))))
+    for l in range(cfg["n_conv_blocks"]):
+        s = cfg["subsample"][l]
+        y = relu(instance_norm(pad_conv(out, w(f"{p}first_conv_layers.{l}.weight"),
+                                        w(f"{p}first_conv_layers.{l}.bias"))))
+        y = relu(instance_norm(pad_conv(y, w(f"{p}second_conv_layers.{l}.weight"),
+                                        w(f"{p}second_conv_layers.{l}.bias"), stride=s)))
+        if s > 1:
+            out = avg_pool_ceil(out, s)
+        out = y + out
+    return pad_conv(out, w(p + "mean_layer.weight"), w(p + "mean_layer.bias"))
+
+
+def pixel_shuffle_1d(x, s):
+    """models.py:33-49: out[b, c, s*w + r] = in[b, s*c + r, w]."""
+    B, C, W = x.shape
+    return x.reshape(B, C // s, s, W).transpose(0, 1, 3, 2).reshape(B, C // s, W * s)
+
+
+def append_cond(x, cond):
+    """models.py:66-79: first half of cond is the mean, second half the std."""
+    p = cond.shape[1] // 2
+    return x * cond[:, p:, None] + cond[:, :p, None]
+
+
+def dec_forward(w, cfg, z, cond, p="decoder."):
+    """Decoder.forward (models.py:403-435), sn=False."""
+    out = relu(instance_norm(pad_conv(z, w(p + "in_conv_layer.weight"), w(p + "in_conv_layer.bias"))))
+    for l in range(cfg["n_conv_blocks"]):
+        up = cfg["upsample"][l]
+        y = instance_norm(pad_conv(out, w(f"{p}first_conv_layers.{l}.weight"), w(f"{p}first_conv_layers.{l}.bias")))
+        y = relu(append_cond(y, linear(cond, w(f"{p}conv_affine_layers.{2*l}.weight"),
+                                       w(f"{p}conv_affine_layers.{2*l}.bias"))))
+        y = pad_conv(y, w(f"{p}second_conv_layers.{l}.weight"), w(f"{p}second_conv_layers.{l}.bias"))
+        if up > 1:
+            y = pixel_shuffle_1d(y, up)
+        y = instance_norm(y)
+        y = relu(append_cond(y, linear(cond, w(f"{p}conv_affine_layers.{2*l+1}.weight"),
+                                       w(f"{p}conv_affine_layers.{2*l+1}.bias"))))
+        out = y + (np.repeat(out, up, axis=2) if up > 1 else out)       # upsample 52-63 (nearest)
+    return pad_conv(out, w(p + "out_conv_layer.weight"), w(p + "out_conv_layer.bias"))
+
+
+def inference(w, cfg, src, tgt):
+    """AdaInVC.inference (models.py:472-485)."""
+    mu = ce_forward(w, cfg["ContentEncoder"], src)
+    emb, _ = se_forward(w, cfg["SpeakerEncoder"], tgt)
+    return dec_forward(w, cfg["Decoder"], mu, emb)
+
+
+# ----------------------------------------------------------------------------------
+# loss + optimiser
+# ----------------------------------------------------------------------------------
+
+
+def emb_loss(emb, tgt, org, n_elems):
+    """attack_utils.py:81 MSE(adv,tgt) - 0.1*MSE(adv,org), mean over n_elems."""
+    d = emb.dtype.type(n_elems)
+    return ((emb - tgt) ** 2).sum(axis=-1) / d - 0.1 * ((emb - org) ** 2).sum(axis=-1) / d
+
+
+def emb_loss_grad(emb, tgt, org, n_elems):
+    """Autograd of nn.MSELoss(mean): 2*(x-y)/N * grad_out, grad_out = 1 and -0.1."""
+    norm = emb.dtype.type(2.0 / n_elems)
+    return norm * (emb - tgt) + norm * (emb - org) * emb.dtype.type(-0.1)
+
+
+class Adam:
+    """torch.optim.Adam defaults (attack_utils.py:69), _single_tensor_adam math:
+    m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+    p.addcdiv_(m, sqrt(v)/sqrt(1-b2^t) + eps, value=-lr/(1-b1^t))."""
+
+    def __init__(self, p, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        self.p = p
+        self.m = np.zeros_like(p)
+        self.v = np.zeros_like(p)
+        self.t = 0
+        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+
+    def step(self, g):
+        ft = self.p.dtype.type
+        self.t += 1
+        self.m += ft(1 - self.b1) * (g - self.m)
+        self.v *= ft(self.b2)
+        self.v += ft(1 - self.b2) * g * g
+        bc1 = 1 - self.b1 ** self.t
+        bc2s = (1 - self.b2 ** self.t) ** 0.5
+        denom = np.sqrt(self.v) / ft(bc2s) + ft(self.eps)
+        self.p += ft(-self.lr / bc1) * (self.m / denom)
+
+
+# ----------------------------------------------------------------------------------
+# attacks
+# ----------------------------------------------------------------------------------
+
+
+def emb_attack(w, cfg, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction="independent",
+               record=None):
+    """emb_attack (attack_utils.py:51-86) with an explicit ptb0.
+
+    reduction="independent": each utterance of the batch is its own attack
+    (loss summed over utterances, each an MSE mean over the embedding); equals
+    B separate reference calls.  reduction="mean": the loss is the reference's
+    MSE mean over the whole [B, D] batch, i.e. the reference called on the
+    batched tensor.  record: optional dict filled with "losses" and "grad0".
+    """
+    se = cfg["SpeakerEncoder"] if "SpeakerEncoder" in cfg else cfg
+    dt = vc_tgt.dtype.type
+    ptb = ptb0.astype(vc_tgt.dtype).copy()
+    opt = Adam(ptb)
+    org, _ = se_forward(w, se, vc_tgt)
+    tgt, _ = se_forward(w, se, adv_tgt)
+    B, D = org.shape
+    n_el = D if reduction == "independent" else B * D
+    losses = []
+    for it in range(n_iters):
+        th = np.tanh(ptb)
+        adv = vc_tgt + dt(eps) * th                                    # attack_utils.py:78
+        emb, st = se_forward(w, se, adv)
+        if record is not None:
+            losses.append(emb_loss(emb, tgt, org, n_el))
+        g_emb = emb_loss_grad(emb, tgt, org, n_el)
+        g_adv = se_backward(w, se, st, g_emb)
+        g = (g_adv * dt(eps)) * (dt(1) - th * th)                       # tanh backward
+        if record is not None and it == 0:
+            record["grad0"] = g.copy()
+        opt.step(g)
+    if record is not None:
+        record["losses"] = np.stack(losses, axis=-1) if losses else None
+    return vc_tgt + dt(eps) * np.tanh(ptb)

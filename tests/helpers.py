@@ -1,0 +1,60 @@
+"""Shared test helpers: models from fixtures, oracle weights, tolerances."""
+import hashlib
+import json
+
+import numpy as np
+import torch
+
+import models
+from oracle import adain_vc as oracle
+
+# Stated fp32 tolerances (calibrated against fp32-vs-fp64 drift of
+# the reference itself).  |adv - ref| is bounded by 2*eps = 0.2 whatever happens,
+# so element checks are only meaningful well below that.
+TOL_SE_REL = 1e-5        # SpeakerEncoder output, relative to max |emb|
+TOL_GRAD_REL = 1e-4      # d loss / d ptb at iteration 0, relative to max |grad|
+# Adam divides each element's step by that element's own gradient RMS, so an
+# element whose gradient nearly cancels amplifies last-bit differences in the
+# summation order: the max is loose, the mean is the sharp check.
+TOL_ADV = {1: 1e-5, 10: 1e-4, 100: 1e-3, 1500: 5e-3}
+TOL_ADV_MEAN = {1: 1e-8, 10: 1e-7, 100: 1e-6, 1500: 1e-4}
+
+
+def check_adv(adv, ref, n):
+    d = np.abs(np.asarray(adv, np.float64) - np.asarray(ref, np.float64))
+    assert d.max() <= TOL_ADV[n], (n, d.max())
+    assert d.mean() <= TOL_ADV_MEAN[n], (n, d.mean())
+
+
+def cfg_of(z):
+    return json.loads(str(z["config"]))
+
+
+def state_of(z):
+    return {k[2:]: torch.from_numpy(np.asarray(z[k])) for k in z if k.startswith("w/")}
+
+
+def model_from_fixture(z):
+    """Small config: weights stored in the fixture. Full config: seeded init,
+    verified against the reference's weight hashes."""
+    cfg = cfg_of(z)
+    if any(k.startswith("w/") for k in z):
+        m = models.AdaInVC(cfg)
+        m.load_state_dict(state_of(z))
+        return m
+    torch.manual_seed(0)
+    m = models.AdaInVC(cfg)
+    hs = json.loads(str(z["weight_sha256"]))
+    for k, v in m.state_dict().items():
+        assert hashlib.sha256(v.numpy().tobytes()).hexdigest() == hs[k], k
+    return m
+
+
+def oracle_weights(m):
+    return oracle.Weights({k: v.detach().cpu().numpy() for k, v in m.state_dict().items()})
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))

@@ -1,0 +1,162 @@
+"""GPU parity: libavc's HIP path vs the reference's golden vectors and the CPU
+oracle, through the C ABI (avc_native -> libavc.so).  All tests need an MI355X."""
+import numpy as np
+import pytest
+import torch
+
+import attack_utils
+import avc_native
+from helpers import TOL_GRAD_REL, TOL_SE_REL, cfg_of, check_adv, model_from_fixture, oracle_weights, rel
+from oracle import adain_vc as oracle
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    avc_native.lib()
+    return DEV
+
+
+@pytest.mark.parametrize("name", ["small_T32", "small_T33", "full_T128", "full_T127"])
+def test_se_forward_golden(gpu, golden, name):
+    z = golden(name)
+    m = model_from_fixture(z).to(gpu)
+    for key, x in (("se_vc_tgt", "vc_tgt"), ("se_adv_tgt", "adv_tgt")):
+        e = m.speaker_encoder(_dev(z[x])).cpu().numpy()
+        assert rel(e, z[key]) <= TOL_SE_REL, (name, key, rel(e, z[key]))
+
+
+@pytest.mark.parametrize("name,ns", [("small_T32", [1, 10, 100]), ("small_T33", [10]),
+                                     ("full_T128", [1, 10, 100, 1500]), ("full_T127", [10])])
+def test_emb_attack_golden(gpu, golden, name, ns):
+    z = golden(name)
+    m = model_from_fixture(z).to(gpu)
+    for n in ns:
+        adv, info = attack_utils.emb_attack(m, _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, n,
+                                            ptb0=_dev(z["emb_ptb0"]), return_info=True)
+        check_adv(adv.detach().cpu().numpy(), z[f"emb_adv_n{n}"], n)
+        g0 = info["grad0"].cpu().numpy()
+        assert rel(g0, z["emb_grad0"]) <= TOL_GRAD_REL, rel(g0, z["emb_grad0"])
+        key = f"emb_losses_n{n}"
+        if key in z:
+            np.testing.assert_allclose(info["losses"].cpu().numpy().T, z[key], rtol=2e-4, atol=1e-8)
+
+
+def test_emb_attack_batched_mean(gpu, golden):
+    z = golden("small_T32")
+    m = model_from_fixture(z).to(gpu)
+    adv = attack_utils.emb_attack(m, _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
+                                  ptb0=_dev(z["emb_batched_ptb0"]), reduction="mean")
+    check_adv(adv.detach().cpu().numpy(), z["emb_batched_adv_n10"], 10)
+
+
+def test_emb_attack_draws_ptb_like_reference(gpu, golden):
+    """Without ptb0, emb_attack consumes the RNG exactly like attack_utils.py:68."""
+    z = golden("small_T32")
+    m = model_from_fixture(z).to(gpu)
+    vc, at = _dev(z["vc_tgt"][:1]), _dev(z["adv_tgt"][:1])
+    torch.manual_seed(7)
+    a = attack_utils.emb_attack(m, vc, at, 0.1, 3)
+    torch.manual_seed(7)
+    p0 = torch.zeros_like(vc).normal_(0, 1)
+    b = attack_utils.emb_attack(m, vc, at, 0.1, 3, ptb0=p0)
+    assert torch.equal(a, b)
+    assert a.requires_grad
+
+
+def test_oracle_parity_random(gpu):
+    """Seeded synthetic inputs at sizes the oracle finishes in seconds; also
+    B not a multiple of the head's 16-utterance tile and an odd T."""
+    cfg = cfg_of_small()
+    torch.manual_seed(3)
+    import models
+    m = models.AdaInVC(cfg)
+    w = oracle_weights(m)
+    m = m.to(gpu)
+    g = torch.Generator().manual_seed(11)
+    B, T = 17, 45
+    vc, at, p0 = (torch.randn(B, 80, T, generator=g) for _ in range(3))
+    e = m.speaker_encoder(vc.to(gpu)).cpu().numpy()
+    eo, _ = oracle.se_forward(w, cfg["SpeakerEncoder"], vc.numpy())
+    assert rel(e, eo) <= TOL_SE_REL
+    adv = attack_utils.emb_attack(m, vc.to(gpu), at.to(gpu), 0.1, 10, ptb0=p0.to(gpu))
+    ref = oracle.emb_attack(w, cfg, vc.numpy(), at.numpy(), 0.1, 10, p0.numpy())
+    check_adv(adv.detach().cpu().numpy(), ref, 10)
+
+
+def cfg_of_small():
+    import json
+    import os
+    from conftest import GOLDEN
+    return json.loads(str(np.load(os.path.join(GOLDEN, "small_T32.npz"))["config"]))
+
+
+def test_minimum_length_and_errors(gpu, golden):
+    z = golden("full_T128")
+    m = model_from_fixture(z).to(gpu)
+    x = torch.randn(2, 80, 9, device=gpu)        # shortest T the full config accepts
+    e = m.speaker_encoder(x)
+    w = oracle_weights(m)
+    eo, _ = oracle.se_forward(w, cfg_of(z)["SpeakerEncoder"], x.cpu().numpy())
+    assert rel(e.cpu().numpy(), eo) <= TOL_SE_REL
+    with pytest.raises(RuntimeError, match="too short"):
+        m.speaker_encoder(torch.randn(1, 80, 8, device=gpu))
+    with pytest.raises(RuntimeError, match="MI355X"):
+        attack_utils.emb_attack(m, torch.randn(1, 80, 32), torch.randn(1, 80, 32), 0.1, 1)
+
+
+def test_batch_shard_invariance(gpu, golden):
+    """Per-utterance independence: attacking a batch equals attacking its two
+    halves separately, bit for bit (what multi-GPU sharding relies on)."""
+    z = golden("full_T128")
+    m = model_from_fixture(z).to(gpu)
+    g = torch.Generator().manual_seed(5)
+    B, T = 48, 128
+    vc, at, p0 = (torch.randn(B, 80, T, generator=g).to(gpu) for _ in range(3))
+    full = attack_utils.emb_attack(m, vc, at, 0.1, 20, ptb0=p0).detach()
+    h = B // 2
+    lo = attack_utils.emb_attack(m, vc[:h], at[:h], 0.1, 20, ptb0=p0[:h]).detach()
+    hi = attack_utils.emb_attack(m, vc[h:], at[h:], 0.1, 20, ptb0=p0[h:]).detach()
+    assert torch.equal(torch.cat([lo, hi]), full)
+
+
+def test_graph_and_eager_agree(gpu, golden):
+    z = golden("small_T32")
+    m = model_from_fixture(z).to(gpu)
+    ctx = avc_native.context_for(m.speaker_encoder, gpu)
+    args = (_dev(z["vc_tgt"]), _dev(z["adv_tgt"]), _dev(z["emb_ptb0"]), 0.1, 25)
+    a, _, _ = ctx.emb_attack(*args, use_graph=True)
+    b, _, _ = ctx.emb_attack(*args, use_graph=False)
+    assert torch.equal(a, b)
+
+
+def test_full_size_properties(gpu, golden):
+    """B=256, T=128 (the bench workload): determinism across calls, the
+    perturbation bound |adv - vc| <= eps, and the embedding loss decreasing."""
+    z = golden("full_T128")
+    m = model_from_fixture(z).to(gpu)
+    g = torch.Generator().manual_seed(1)
+    B, T = 256, 128
+    vc, at = (torch.randn(B, 80, T, generator=g).to(gpu) for _ in range(2))
+    p0 = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(123)).to(gpu)
+    a, info = attack_utils.emb_attack(m, vc, at, 0.1, 50, ptb0=p0, return_info=True)
+    b = attack_utils.emb_attack(m, vc, at, 0.1, 50, ptb0=p0)
+    assert torch.equal(a, b)
+    assert float((a - vc).abs().max()) <= 0.1 + 1e-6
+    L = info["losses"].cpu().numpy()
+    assert np.all(L[-1] < L[0])
+    # spot-check 2 utterances of the batch against the oracle
+    w = oracle_weights(m)
+    idx = [0, 255]
+    ref = oracle.emb_attack(w, cfg_of(z), vc[idx].cpu().numpy(), at[idx].cpu().numpy(), 0.1, 50,
+                            p0[idx].cpu().numpy())
+    d = np.abs(a[idx].detach().cpu().numpy() - ref)
+    assert d.max() <= 1e-3 and d.mean() <= 1e-6

@@ -1,0 +1,115 @@
+"""CPU: pin the numpy oracle (oracle/adain_vc.py) against vectors produced by the
+real reference (tests/golden/make_golden.py), and pin our AdaInVC parameter
+tree / seeded init against the reference's (weight hashes)."""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import models
+from helpers import TOL_GRAD_REL, TOL_SE_REL, cfg_of, check_adv, model_from_fixture, oracle_weights, rel
+from oracle import adain_vc as oracle
+
+
+@pytest.mark.parametrize("name", ["small_T32", "small_T33", "full_T128", "full_T127"])
+def test_speaker_encoder_forward(golden, name):
+    z = golden(name)
+    m = model_from_fixture(z)
+    w = oracle_weights(m)
+    se = cfg_of(z)["SpeakerEncoder"]
+    for key, x in (("se_vc_tgt", "vc_tgt"), ("se_adv_tgt", "adv_tgt")):
+        e, _ = oracle.se_forward(w, se, z[x])
+        assert rel(e, z[key]) <= TOL_SE_REL
+
+
+@pytest.mark.parametrize("name", ["small_T32", "small_T33", "full_T128", "full_T127"])
+def test_inference_forward(golden, name):
+    z = golden(name)
+    w = oracle_weights(model_from_fixture(z))
+    out = oracle.inference(w, cfg_of(z), z["vc_src"], z["vc_tgt"])
+    assert rel(out, z["inference"]) <= 1e-5
+
+
+@pytest.mark.parametrize("name,ns", [("small_T32", [1, 10, 100]), ("small_T33", [10]),
+                                     ("full_T128", [1, 10]), ("full_T127", [10])])
+def test_emb_attack(golden, name, ns):
+    z = golden(name)
+    w = oracle_weights(model_from_fixture(z))
+    cfg = cfg_of(z)
+    for n in ns:
+        rec = {}
+        adv = oracle.emb_attack(w, cfg, z["vc_tgt"], z["adv_tgt"], 0.1, n, z["emb_ptb0"], record=rec)
+        check_adv(adv, z[f"emb_adv_n{n}"], n)
+        assert rel(rec["grad0"], z["emb_grad0"]) <= TOL_GRAD_REL
+        if f"emb_losses_n{n}" in z:
+            np.testing.assert_allclose(rec["losses"], z[f"emb_losses_n{n}"], rtol=1e-4, atol=1e-9)
+
+
+def test_emb_attack_batched_mean(golden):
+    """The reference called on a [2,80,T] tensor == reduction="mean"."""
+    z = golden("small_T32")
+    w = oracle_weights(model_from_fixture(z))
+    adv = oracle.emb_attack(w, cfg_of(z), z["vc_tgt"], z["adv_tgt"], 0.1, 10, z["emb_batched_ptb0"],
+                            reduction="mean")
+    check_adv(adv, z["emb_batched_adv_n10"], 10)
+
+
+@pytest.mark.slow
+def test_emb_attack_full_n100(golden):
+    z = golden("full_T128")
+    w = oracle_weights(model_from_fixture(z))
+    adv = oracle.emb_attack(w, cfg_of(z), z["vc_tgt"], z["adv_tgt"], 0.1, 100, z["emb_ptb0"])
+    check_adv(adv, z["emb_adv_n100"], 100)
+
+
+def test_seeded_init_matches_reference(golden):
+    """Our module tree draws the reference's default-init weights bit for bit."""
+    z = golden("full_T128")
+    hs = json.loads(str(z["weight_sha256"]))
+    torch.manual_seed(0)
+    sd = models.AdaInVC(cfg_of(z)).state_dict()
+    assert list(sd.keys()) == list(hs.keys())
+    for k, v in sd.items():
+        assert hashlib.sha256(v.numpy().tobytes()).hexdigest() == hs[k], k
+
+
+def test_small_state_dict_layout(golden):
+    z = golden("small_T32")
+    m = models.AdaInVC(cfg_of(z))
+    keys = [k[2:] for k in z if k.startswith("w/")]
+    assert list(m.state_dict().keys()) == keys
+    for k, v in m.state_dict().items():
+        assert tuple(v.shape) == z["w/" + k].shape
+
+
+def test_pool_ceil_mode_edge():
+    """F.avg_pool1d(k=2, ceil_mode=True) on [0..4] -> [0.5, 2.5, 4.0]."""
+    x = np.arange(5, dtype=np.float32)[None, None, :]
+    np.testing.assert_array_equal(oracle.avg_pool_ceil(x, 2)[0, 0], [0.5, 2.5, 4.0])
+
+
+def test_reflect_pad_adjoint():
+    """<P x, y> == <x, P^T y> for every bank/conv pad pair."""
+    rng = np.random.default_rng(0)
+    for k in range(1, 9):
+        pl, pr = oracle.bank_pads(k)
+        x = rng.standard_normal((2, 3, 11))
+        y = rng.standard_normal((2, 3, 11 + pl + pr))
+        lhs = (oracle.reflect_pad(x, pl, pr) * y).sum()
+        rhs = (x * oracle.reflect_pad_backward(y, pl, pr, 11)).sum()
+        assert abs(lhs - rhs) < 1e-9
+
+
+def test_torch_cpu_baseline_is_reference_arithmetic(golden):
+    """bench.py's CPU baseline (oracle/torch_cpu.py) reproduces the reference bitwise."""
+    from oracle import torch_cpu
+    z = golden("small_T32")
+    m = model_from_fixture(z)
+    sd = m.state_dict()
+    for b in range(2):
+        out = torch_cpu.emb_attack(sd, cfg_of(z), torch.from_numpy(z["vc_tgt"][b:b + 1]),
+                                   torch.from_numpy(z["adv_tgt"][b:b + 1]), 0.1, 10,
+                                   torch.from_numpy(z["emb_ptb0"][b:b + 1]))
+        assert torch.equal(out, torch.from_numpy(z["emb_adv_n10"][b:b + 1]))
