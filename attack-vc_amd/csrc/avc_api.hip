@@ -16,7 +16,7 @@
 #include "avc_kernels.h"
 
 namespace avc {
-template <int WM, int WN>
+template <int WM, int WN, int KC, int MODE, int STRIDE>
 __global__ void conv_gemm_f32(const Problem* __restrict__ probs);
 __global__ void se_head(HeadArgs A);
 __global__ void attack_init(const float* vc, const float* ptb0, float* ptb, float* m, float* v, float* adv,
@@ -61,10 +61,26 @@ struct HostConv {
     const float* b;
 };
 
-enum LaunchKind { L_GEMM22, L_GEMM21, L_GEMM11, L_HEAD, L_INIT };
+enum LaunchKind { L_GEMM, L_HEAD };
+
+// conv_gemm_f32 instantiations (tile = 64*WM x 64*WN, K chunk KC); the planner
+// autotunes one per launch on first use of a workspace.
+struct Variant {
+    int wm, wn, kc;
+    const char* name;
+};
+static const Variant VARIANTS[] = {
+    {2, 2, 32, "conv_gemm_f32<128x128,k32>"}, {2, 2, 16, "conv_gemm_f32<128x128,k16>"},
+    {2, 1, 32, "conv_gemm_f32<128x64,k32>"},  {1, 1, 32, "conv_gemm_f32<64x64,k32>"},
+    {1, 1, 16, "conv_gemm_f32<64x64,k16>"},
+};
+constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
 struct Launch {
     int kind;
+    int variant = 0;             // L_GEMM: index into VARIANTS
+    int mode = 0, stride = 1;    // L_GEMM: loader specialisation shared by all its problems
+    int maxM = 0, maxN = 0;      // L_GEMM: grid extents over its problems
     dim3 grid, block;
     size_t shmem = 0;
     Problem* dprobs = nullptr;   // device problem table (L_GEMM*)
@@ -82,7 +98,7 @@ struct Plan {
 struct Workspace {
     int B = 0, T = 0;
     std::vector<int> Tl;        // T_0..T_n (per conv block input lengths)
-    DevBuf xin, adv, vc, ptb, m, v, bank, h0, gbank, gxd, g1, ghx, ghy, emb_fwd, org, tgt, grad0;
+    DevBuf xin, adv, vc, ptb, m, v, bank, h0, gbank, gxd, g1, ghx, ghy, gmx, gmy, emb_fwd, org, tgt, grad0;
     std::vector<DevBuf> a1, a2, hb;   // per block
     DevBuf losses, table, scal;
     int iters_cap = 0;
@@ -137,6 +153,14 @@ static void dfree(DevBuf& b) {
     b.n = 0;
 }
 
+// A matrices ([K][Mpad]) get zero rows up to a multiple of KALIGN so every K chunk
+// size the kernels use reads in bounds.
+static std::vector<float> pad_rows(std::vector<float> At, int Mpad) {
+    const size_t rows = At.size() / Mpad;
+    At.resize((size_t)rup((int)rows, KALIGN) * Mpad, 0.f);
+    return At;
+}
+
 static int upload(DevBuf& b, const std::vector<float>& h) {
     if (dalloc(b, h.size())) return 1;
     HIPCHK(hipMemcpy(b.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
@@ -152,7 +176,7 @@ static void pads_of(int k, int& pl, int& pr) {   // models.py:23-27
 static std::vector<float> pack_fwd(const HostConv& c, int Mpad, int row_base = 0, int Krows = -1,
                                    std::vector<float>* into = nullptr, int ci_lo = 0, int ci_n = -1) {
     if (ci_n < 0) ci_n = c.ci;
-    const int K = Krows < 0 ? rup(ci_n * c.k, KC) : Krows;
+    const int K = Krows < 0 ? rup(ci_n * c.k, KSEG) : Krows;
     std::vector<float> local;
     std::vector<float>& At = into ? *into : local;
     if (!into) At.assign((size_t)K * Mpad, 0.f);
@@ -285,22 +309,22 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
     ctx->AtF_bank.resize(nb);
     ctx->bias_bank.resize(nb);
     for (int i = 0; i < nb; ++i) {
-        up(ctx->AtF_bank[i], pack_fwd(bank[i], MpadB));
+        up(ctx->AtF_bank[i], pad_rows(pack_fwd(bank[i], MpadB), MpadB));
         upv(ctx->bias_bank[i], bank[i].b, c.c_bank);
     }
     {
         const int MpadH = rup(c.c_h, 128);
-        const int k1 = rup(c.c_bank * nb, KC), k2 = rup(c.c_in, KC);
+        const int k1 = rup(c.c_bank * nb, KSEG), k2 = rup(c.c_in, KSEG);
         std::vector<float> At((size_t)(k1 + k2) * MpadH, 0.f);
         pack_fwd(inc, MpadH, 0, k1 + k2, &At, 0, c.c_bank * nb);
         pack_fwd(inc, MpadH, k1, k1 + k2, &At, c.c_bank * nb, c.c_in);
-        up(ctx->AtF_in, At);
+        up(ctx->AtF_in, pad_rows(At, MpadH));
         upv(ctx->bias_in, inc.b, c.c_h);
         // in_conv dgrad: M = cin_cat rows (ci), K = c_h (co): At[co][ci] = W[co][ci]
         const int MpadI = rup(cin_cat, 128);
-        std::vector<float> Bt((size_t)rup(c.c_h, KC) * MpadI, 0.f);
+        std::vector<float> Bt((size_t)rup(c.c_h, KSEG) * MpadI, 0.f);
         pack_bwd(inc, MpadI, 0, Bt);
-        up(ctx->AtB_in, Bt);
+        up(ctx->AtB_in, pad_rows(Bt, MpadI));
     }
     ctx->AtF_c1.resize(c.n_conv_blocks);
     ctx->AtF_c2.resize(c.n_conv_blocks);
@@ -310,14 +334,14 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
     ctx->bias_c2.resize(c.n_conv_blocks);
     for (int l = 0; l < c.n_conv_blocks; ++l) {
         const int MpadH = rup(c.c_h, 128);
-        up(ctx->AtF_c1[l], pack_fwd(c1[l], MpadH));
-        up(ctx->AtF_c2[l], pack_fwd(c2[l], MpadH));
-        const int Kb = rup(c.c_h * c.kernel_size, KC);
+        up(ctx->AtF_c1[l], pad_rows(pack_fwd(c1[l], MpadH), MpadH));
+        up(ctx->AtF_c2[l], pad_rows(pack_fwd(c2[l], MpadH), MpadH));
+        const int Kb = rup(c.c_h * c.kernel_size, KSEG);
         std::vector<float> b1((size_t)Kb * MpadH, 0.f), b2((size_t)Kb * MpadH, 0.f);
         pack_bwd(c1[l], MpadH, 0, b1);
         pack_bwd(c2[l], MpadH, 0, b2);
-        up(ctx->AtB_c1[l], b1);
-        up(ctx->AtB_c2[l], b2);
+        up(ctx->AtB_c1[l], pad_rows(b1, MpadH));
+        up(ctx->AtB_c2[l], pad_rows(b2, MpadH));
         upv(ctx->bias_c1[l], c1[l].b, c.c_h);
         upv(ctx->bias_c2[l], c2[l].b, c.c_h);
     }
@@ -325,7 +349,7 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
         const int MpadX = rup(c.c_in, 128);
         int Ktot = 0;
         for (int i = 0; i < nb; ++i) {
-            ctx->kpadB_bank.push_back(rup(c.c_bank * ctx->bank_k[i], KC));
+            ctx->kpadB_bank.push_back(rup(c.c_bank * ctx->bank_k[i], KSEG));
             Ktot += ctx->kpadB_bank.back();
         }
         std::vector<float> At((size_t)Ktot * MpadX, 0.f);
@@ -334,7 +358,7 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
             pack_bwd(bank[i], MpadX, row, At);
             row += ctx->kpadB_bank[i];
         }
-        up(ctx->AtB_bank, At);
+        up(ctx->AtB_bank, pad_rows(At, MpadX));
     }
     {   // head
         const size_t CC = (size_t)c.c_h * c.c_h;
@@ -384,7 +408,7 @@ static void free_ws(Workspace& ws) {
     free_plan(ws.fwd);
     free_plan(ws.iter);
     DevBuf* bufs[] = {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.bank, &ws.h0, &ws.gbank, &ws.gxd,
-                      &ws.g1, &ws.ghx, &ws.ghy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal};
+                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal};
     for (DevBuf* b : bufs) dfree(*b);
     for (auto& b : ws.a1) dfree(b);
     for (auto& b : ws.a2) dfree(b);
@@ -420,13 +444,12 @@ extern "C" void avc_destroy(avc_ctx* ctx) {
 // planning
 // ---------------------------------------------------------------------------------
 
-static Seg make_seg(const float* src, const float* mask, int k0, int C, int c_off, int src_C, int src_T, int ks,
-                    int stride, int pl, int pr, int mode) {
+static Seg make_seg(const float* src, int k0, int C, int c_off, int src_C, int src_T, int ks, int stride, int pl,
+                    int pr, int mode) {
     Seg s{};
     s.src = src;
-    s.mask = mask;
     s.k0 = k0;
-    s.kpad = rup(C * ks, KC);
+    s.kpad = rup(C * ks, KSEG);
     s.C = C;
     s.c_off = c_off;
     s.src_C = src_C;
@@ -456,43 +479,50 @@ static void add_seg(Problem& p, const Seg& s) {
     p.K = s.k0 + s.kpad;
 }
 
-// choose the tile so a launch has enough workgroups to fill 256 CUs
-static int pick_tile(const std::vector<Problem>& ps) {
+static dim3 gemm_grid(const Launch& L) {
+    const Variant& v = VARIANTS[L.variant];
+    return dim3(cdiv(L.maxN, 64 * v.wn), cdiv(L.maxM, 64 * v.wm), L.nprob);
+}
+
+// default tile before autotuning: enough workgroups to fill 256 CUs
+static int default_variant(const std::vector<Problem>& ps) {
     auto count = [&](int MT, int NT) {
         long n = 0;
         for (auto& p : ps) n += (long)cdiv(p.M, MT) * cdiv(p.N, NT);
         return n;
     };
-    if (count(128, 128) >= 1024) return L_GEMM22;
-    if (count(128, 64) >= 768) return L_GEMM21;
-    return L_GEMM11;
+    if (count(128, 128) >= 512) return 0;
+    if (count(128, 64) >= 512) return 2;
+    return 3;
 }
 
 static int add_gemm(Plan& pl, std::vector<Problem> ps, double flop, const char* what) {
-    const int kind = pick_tile(ps);
-    const int MT = kind == L_GEMM11 ? 64 : 128;
-    const int NT = kind == L_GEMM22 ? 128 : 64;
     int gx = 0, gy = 0;
     for (auto& p : ps) {
-        if (p.K % KC) return fail("internal: K %d not a multiple of %d", p.K, KC);
-        if (p.Mpad % MT) return fail("internal: Mpad %d not a multiple of %d", p.Mpad, MT);
-        gx = std::max(gx, cdiv(p.N, NT));
-        gy = std::max(gy, cdiv(p.M, MT));
+        for (int i = 0; i < p.nseg; ++i)
+            if (p.seg[i].mode != ps[0].seg[0].mode || p.seg[i].stride != ps[0].seg[0].stride)
+                return fail("internal: mixed loader modes in one launch");
+        if (p.K % KSEG) return fail("internal: K %d not a multiple of %d", p.K, KSEG);
+        if (p.Mpad % 128) return fail("internal: Mpad %d not a multiple of 128", p.Mpad);
+        gx = std::max(gx, p.N);
+        gy = std::max(gy, p.M);
     }
     Problem* d = nullptr;
     HIPCHK(hipMalloc(&d, ps.size() * sizeof(Problem)));
     HIPCHK(hipMemcpy(d, ps.data(), ps.size() * sizeof(Problem), hipMemcpyHostToDevice));
     pl.owned.push_back(d);
     Launch L;
-    L.kind = kind;
-    L.grid = dim3(gx, gy, (unsigned)ps.size());
+    L.kind = L_GEMM;
+    L.variant = default_variant(ps);
+    L.mode = ps[0].seg[0].mode;
+    L.stride = ps[0].seg[0].stride;
+    L.maxN = gx;
+    L.maxM = gy;
     L.block = dim3(256);
     L.dprobs = d;
     L.nprob = (int)ps.size();
     L.flop = flop;
-    static const char* names[] = {"conv_gemm_f32<2,2>", "conv_gemm_f32<2,1>", "conv_gemm_f32<1,1>"};
-    L.name = names[kind];
-    (void)what;
+    L.name = what;
     pl.launches.push_back(L);
     return 0;
 }
@@ -511,7 +541,7 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
             pads_of(k, pl_, pr_);
             Problem p = base_problem(c.c_bank, rup(c.c_bank, 128), N0, T, ctx->AtF_bank[i].p, ctx->bias_bank[i].p,
                                      c.act);
-            add_seg(p, make_seg(x, nullptr, 0, c.c_in, 0, c.c_in, T, k, 1, pl_, pr_, SEG_FWD));
+            add_seg(p, make_seg(x, 0, c.c_in, 0, c.c_in, T, k, 1, pl_, pr_, SEG_FWD));
             p.epi = EPI_ACT;
             p.out0 = ws.bank.p;
             p.out0_C = nb * c.c_bank;
@@ -524,8 +554,8 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
     }
     {   // in_conv_layer over cat(bank, x) (models.py:103,337-338)
         Problem p = base_problem(c.c_h, rup(c.c_h, 128), N0, T, ctx->AtF_in.p, ctx->bias_in.p, c.act);
-        add_seg(p, make_seg(ws.bank.p, nullptr, 0, nb * c.c_bank, 0, nb * c.c_bank, T, 1, 1, 0, 0, SEG_FWD));
-        add_seg(p, make_seg(x, nullptr, p.K, c.c_in, 0, c.c_in, T, 1, 1, 0, 0, SEG_FWD));
+        add_seg(p, make_seg(ws.bank.p, 0, nb * c.c_bank, 0, nb * c.c_bank, T, 1, 1, 0, 0, SEG_FWD));
+        add_seg(p, make_seg(x, p.K, c.c_in, 0, c.c_in, T, 1, 1, 0, 0, SEG_FWD));
         p.epi = EPI_ACT;
         p.out0 = ws.h0.p;
         p.out0_C = c.c_h;
@@ -537,13 +567,13 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
         const int Ti = ws.Tl[l], To = ws.Tl[l + 1], s = c.subsample[l];
         const float* hin = l == 0 ? ws.h0.p : ws.hb[l - 1].p;
         Problem p1 = base_problem(c.c_h, rup(c.c_h, 128), B * Ti, Ti, ctx->AtF_c1[l].p, ctx->bias_c1[l].p, c.act);
-        add_seg(p1, make_seg(hin, nullptr, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, 1, kpl, kpr, SEG_FWD));
+        add_seg(p1, make_seg(hin, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, 1, kpl, kpr, SEG_FWD));
         p1.epi = EPI_ACT;
         p1.out0 = ws.a1[l].p;
         p1.out0_C = c.c_h;
         if (add_gemm(pl, {p1}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * Ti, "conv1")) return 1;
         Problem p2 = base_problem(c.c_h, rup(c.c_h, 128), B * To, To, ctx->AtF_c2[l].p, ctx->bias_c2[l].p, c.act);
-        add_seg(p2, make_seg(ws.a1[l].p, nullptr, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, s, kpl, kpr, SEG_FWD));
+        add_seg(p2, make_seg(ws.a1[l].p, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, s, kpl, kpr, SEG_FWD));
         p2.epi = EPI_BLOCK;
         p2.out0 = ws.a2[l].p;
         p2.out0_C = c.c_h;
@@ -565,6 +595,8 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
         HeadArgs& A = L.head;
         A.hN = c.n_conv_blocks ? ws.hb[c.n_conv_blocks - 1].p : ws.h0.p;
         A.g_hN = ws.ghx.p;
+        A.g_hN_masked = ws.gmx.p;   // dY of the last block's conv2 dgrad: g * act'(a2_last)
+        A.mask_hN = c.n_conv_blocks ? ws.a2[c.n_conv_blocks - 1].p : ws.h0.p;
         A.Wp = ctx->head_Wp.p;
         A.WpT = ctx->head_WpT.p;
         A.bias = ctx->head_bias.p;
@@ -581,6 +613,7 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
         A.act = c.act;
         A.mode = attack ? 1 : 0;
         A.scal = ws.scal.p;
+        A.loss_len = ws.iters_cap;
         const double dense = 2.0 * c.c_h * c.c_h * 2 * c.n_dense_blocks + 2.0 * c.c_out * c.c_h;
         L.flop = dense * B * (attack ? 2 : 1);
         L.name = "se_head";
@@ -595,15 +628,19 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
     const int B = ws.B, T = ws.T, nb = ctx->nb;
     int kpl, kpr;
     pads_of(c.kernel_size, kpl, kpr);
-    // gh ping-pong: head wrote g(h_N) into ghx
+    // g(h_l) ping-pong (unmasked: feeds the residual avg-pool^T) and its ReLU'-masked
+    // copy (the dY of the next dgrad).  The head wrote g(h_N) -> ghx, masked -> gmx.
     DevBuf* gcur = &ws.ghx;
     DevBuf* gnext = &ws.ghy;
+    DevBuf* mcur = &ws.gmx;
+    DevBuf* mnext = &ws.gmy;
     const int MpadH = rup(c.c_h, 128);
     for (int l = c.n_conv_blocks - 1; l >= 0; --l) {
         const int Ti = ws.Tl[l], To = ws.Tl[l + 1], s = c.subsample[l];
-        // conv2^T: dY = g(h_{l+1}) * act'(a2_l), stride s, then * act'(a1_l)
+        // conv2^T: dY = g(h_{l+1}) * act'(a2_l) (masked by its producer), stride s; * act'(a1_l)
         Problem p2 = base_problem(c.c_h, MpadH, B * Ti, Ti, ctx->AtB_c2[l].p, nullptr, c.act);
-        add_seg(p2, make_seg(gcur->p, ws.a2[l].p, 0, c.c_h, 0, c.c_h, To, c.kernel_size, s, kpl, kpr, SEG_BWD));
+        add_seg(p2, make_seg(mcur->p, 0, c.c_h, 0, c.c_h, To, c.kernel_size, s, kpl, kpr, SEG_BWD));
+        p2.both_edges = Ti <= kpl + kpr + 1;
         p2.epi = EPI_MASK;
         p2.out0 = ws.g1.p;
         p2.out0_C = c.c_h;
@@ -611,24 +648,30 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
         p2.aux0_C = c.c_h;
         p2.aux0_T = Ti;
         if (add_gemm(pl, {p2}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * To, "conv2_dgrad")) return 1;
-        // conv1^T + residual avg-pool^T
+        // conv1^T + residual avg-pool^T -> g(h_l), and its copy masked by the ReLU that
+        // produced h_l (a2_{l-1}, or h0's in_conv ReLU for l = 0)
         Problem p1 = base_problem(c.c_h, MpadH, B * Ti, Ti, ctx->AtB_c1[l].p, nullptr, c.act);
-        add_seg(p1, make_seg(ws.g1.p, nullptr, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, 1, kpl, kpr, SEG_BWD));
+        add_seg(p1, make_seg(ws.g1.p, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, 1, kpl, kpr, SEG_BWD));
+        p1.both_edges = Ti <= kpl + kpr + 1;
         p1.epi = EPI_POOLT;
-        p1.out0 = gnext->p;
+        p1.out0 = l > 0 ? gnext->p : nullptr;
         p1.out0_C = c.c_h;
+        p1.out1 = mnext->p;
+        p1.out1_C = c.c_h;
+        p1.aux1 = l > 0 ? ws.a2[l - 1].p : ws.h0.p;
         p1.aux0 = gcur->p;
         p1.aux0_C = c.c_h;
         p1.aux0_T = To;
         p1.pool_s = s;
         if (add_gemm(pl, {p1}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * Ti, "conv1_dgrad")) return 1;
         std::swap(gcur, gnext);
+        std::swap(mcur, mnext);
     }
     const int N0 = B * T;
     const int cin_cat = nb * c.c_bank + c.c_in;
     {   // in_conv^T: rows = cat channels; dY = g(h0) * act'(h0)
         Problem p = base_problem(cin_cat, rup(cin_cat, 128), N0, T, ctx->AtB_in.p, nullptr, c.act);
-        add_seg(p, make_seg(gcur->p, ws.h0.p, 0, c.c_h, 0, c.c_h, T, 1, 1, 0, 0, SEG_BWD));
+        add_seg(p, make_seg(mcur->p, 0, c.c_h, 0, c.c_h, T, 1, 1, 0, 0, SEG_BWD));
         p.epi = EPI_INCONV_T;
         p.split = nb * c.c_bank;
         p.out0 = ws.gbank.p;
@@ -648,16 +691,18 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
             const int k = ctx->bank_k[i];
             int pl_, pr_;
             pads_of(k, pl_, pr_);
-            add_seg(p, make_seg(ws.gbank.p, nullptr, k0, c.c_bank, i * c.c_bank, nb * c.c_bank, T, k, 1, pl_, pr_,
+            add_seg(p, make_seg(ws.gbank.p, k0, c.c_bank, i * c.c_bank, nb * c.c_bank, T, k, 1, pl_, pr_,
                                 SEG_BWD));
             k0 += ctx->kpadB_bank[i];
             flop += 2.0 * c.c_bank * c.c_in * k * N0;
+            if (T <= pl_ + pr_ + 1) p.both_edges = 1;
         }
         if (nb > MAX_SEGS) return fail("bank_size/bank_scale > %d kernels not supported", MAX_SEGS);
         p.epi = EPI_ADAM;
         p.aux0 = ws.gxd.p;
         p.step = ws.step;
         p.scal = ws.scal.p;
+        p.table_len = ws.iters_cap;
         AdamArgs& A = p.adam;
         A.ptb = ws.ptb.p;
         A.m = ws.m.p;
@@ -674,6 +719,8 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
     }
     return 0;
 }
+
+static int autotune(avc_ctx* ctx, Plan& pl);
 
 static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     Workspace& ws = ctx->ws;
@@ -715,7 +762,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         rc |= dalloc(ws.bank, (size_t)B * nb * c.c_bank * T);
         rc |= dalloc(ws.gbank, (size_t)B * nb * c.c_bank * T);
         const size_t H = (size_t)B * c.c_h * T;
-        for (DevBuf* b : {&ws.h0, &ws.g1, &ws.ghx, &ws.ghy}) rc |= dalloc(*b, H);
+        for (DevBuf* b : {&ws.h0, &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy}) rc |= dalloc(*b, H);
         for (DevBuf* b : {&ws.emb_fwd, &ws.org, &ws.tgt}) rc |= dalloc(*b, (size_t)B * c.c_out);
         ws.a1.resize(c.n_conv_blocks);
         ws.a2.resize(c.n_conv_blocks);
@@ -741,28 +788,136 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     if (plan_forward(ctx, ws, ws.fwd, ws.xin.p, false)) return 1;
     if (plan_forward(ctx, ws, ws.iter, ws.adv.p, true)) return 1;
     if (plan_backward(ctx, ws, ws.iter)) return 1;
+    // autotune with a valid Adam step (1) and eps/gscale (the kernels clamp anyway)
+    const float scal0[4] = {0.1f, 0.f, 0.f, 0.f};
+    HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(ws.step, 0, sizeof(int)));
+    if (autotune(ctx, ws.fwd) || autotune(ctx, ws.iter)) return 1;
     ws.built = true;
     return 0;
 }
 
-static hipError_t launch_one(const Launch& L, hipStream_t s) {
-    switch (L.kind) {
-    case L_GEMM22:
-        hipLaunchKernelGGL((conv_gemm_f32<2, 2>), L.grid, L.block, 0, s, L.dprobs);
-        break;
-    case L_GEMM21:
-        hipLaunchKernelGGL((conv_gemm_f32<2, 1>), L.grid, L.block, 0, s, L.dprobs);
-        break;
-    case L_GEMM11:
-        hipLaunchKernelGGL((conv_gemm_f32<1, 1>), L.grid, L.block, 0, s, L.dprobs);
-        break;
-    case L_HEAD:
-        hipLaunchKernelGGL(se_head, L.grid, L.block, L.shmem, s, L.head);
-        break;
-    default:
-        break;
+template <int WM, int WN, int KC>
+static void launch_tile(const Launch& L, dim3 g, hipStream_t s) {
+    const int st = (L.stride == 1 || L.stride == 2) ? L.stride : 0;
+    if (L.mode == SEG_FWD) {
+        if (st == 1) hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_FWD, 1>), g, L.block, 0, s, L.dprobs);
+        else if (st == 2) hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_FWD, 2>), g, L.block, 0, s, L.dprobs);
+        else hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_FWD, 0>), g, L.block, 0, s, L.dprobs);
+    } else {
+        if (st == 1) hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_BWD, 1>), g, L.block, 0, s, L.dprobs);
+        else if (st == 2) hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_BWD, 2>), g, L.block, 0, s, L.dprobs);
+        else hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_BWD, 0>), g, L.block, 0, s, L.dprobs);
+    }
+}
+
+static hipError_t launch_gemm(const Launch& L, int variant, hipStream_t s) {
+    Launch V = L;
+    V.variant = variant;
+    const dim3 g = gemm_grid(V);
+    switch (variant) {
+    case 0: launch_tile<2, 2, 32>(L, g, s); break;
+    case 1: launch_tile<2, 2, 16>(L, g, s); break;
+    case 2: launch_tile<2, 1, 32>(L, g, s); break;
+    case 3: launch_tile<1, 1, 32>(L, g, s); break;
+    case 4: launch_tile<1, 1, 16>(L, g, s); break;
+    default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+static hipError_t launch_one(const Launch& L, hipStream_t s) {
+    switch (L.kind) {
+    case L_GEMM:
+        return launch_gemm(L, L.variant, s);
+    case L_HEAD:
+        hipLaunchKernelGGL(se_head, L.grid, L.block, L.shmem, s, L.head);
+        return hipGetLastError();
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
+static std::string kernel_name(const Launch& L) {
+    return L.kind == L_GEMM ? std::string(VARIANTS[L.variant].name) : L.name;
+}
+
+// Time every tile variant of every GEMM launch of `pl` on the ctx stream and keep
+// the fastest (median of 3 after a warm-up).  Runs once per workspace build.
+// Tune cache (AVC_TUNE_FILE): lines "key variant" so a profiled re-run (rocprofv3)
+// replays the same tile choices without the tuning launches.
+static std::string tune_key(avc_ctx* ctx, const Plan& pl, size_t li) {
+    char buf[256];
+    const avc_se_cfg& c = ctx->cfg;
+    snprintf(buf, sizeof(buf), "B%d_T%d_ch%d_%d_%d_nb%d_%s_l%zu", ctx->ws.B, ctx->ws.T, c.c_in, c.c_h, c.c_bank,
+             c.n_conv_blocks, &pl == &ctx->ws.fwd ? "fwd" : "iter", li);
+    return buf;
+}
+
+static std::map<std::string, int> read_tune_file() {
+    std::map<std::string, int> m;
+    const char* path = getenv("AVC_TUNE_FILE");
+    if (!path) return m;
+    FILE* f = fopen(path, "r");
+    if (!f) return m;
+    char key[256];
+    int v;
+    while (fscanf(f, "%255s %d", key, &v) == 2) m[key] = v;
+    fclose(f);
+    return m;
+}
+
+static int autotune(avc_ctx* ctx, Plan& pl) {
+    const char* env = getenv("AVC_AUTOTUNE");
+    if (env && env[0] == '0') return 0;
+    std::map<std::string, int> cache = read_tune_file();
+    bool all_cached = true;
+    for (size_t li = 0; li < pl.launches.size(); ++li) {
+        if (pl.launches[li].kind != L_GEMM) continue;
+        auto it = cache.find(tune_key(ctx, pl, li));
+        if (it == cache.end() || it->second < 0 || it->second >= NVARIANTS) all_cached = false;
+    }
+    if (all_cached) {
+        for (size_t li = 0; li < pl.launches.size(); ++li)
+            if (pl.launches[li].kind == L_GEMM) pl.launches[li].variant = cache[tune_key(ctx, pl, li)];
+        return 0;
+    }
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    for (Launch& L : pl.launches) {
+        if (L.kind != L_GEMM) continue;
+        int best = L.variant;
+        float best_ms = 1e30f;
+        for (int v = 0; v < NVARIANTS; ++v) {
+            float t[3];
+            HIPCHK(launch_gemm(L, v, ctx->stream));
+            for (int r = 0; r < 3; ++r) {
+                HIPCHK(hipEventRecord(a, ctx->stream));
+                HIPCHK(launch_gemm(L, v, ctx->stream));
+                HIPCHK(hipEventRecord(b, ctx->stream));
+                HIPCHK(hipEventSynchronize(b));
+                HIPCHK(hipEventElapsedTime(&t[r], a, b));
+            }
+            std::sort(t, t + 3);
+            if (t[1] < best_ms) {
+                best_ms = t[1];
+                best = v;
+            }
+        }
+        L.variant = best;
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (const char* path = getenv("AVC_TUNE_FILE")) {
+        if (FILE* f = fopen(path, "a")) {
+            for (size_t li = 0; li < pl.launches.size(); ++li)
+                if (pl.launches[li].kind == L_GEMM)
+                    fprintf(f, "%s %d\n", tune_key(ctx, pl, li).c_str(), pl.launches[li].variant);
+            fclose(f);
+        }
+    }
+    return 0;
 }
 
 static int run_plan(avc_ctx* ctx, const Plan& pl, bool prof) {
@@ -774,16 +929,17 @@ static int run_plan(avc_ctx* ctx, const Plan& pl, bool prof) {
             HIPCHK(hipEventRecord(a, ctx->stream));
         }
         hipError_t e = launch_one(L, ctx->stream);
-        if (e != hipSuccess) return fail("launch %s: %s", L.name.c_str(), hipGetErrorString(e));
+        if (e != hipSuccess) return fail("launch %s: %s", kernel_name(L).c_str(), hipGetErrorString(e));
         if (prof) {
             HIPCHK(hipEventRecord(b, ctx->stream));
             HIPCHK(hipEventSynchronize(b));
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, a, b));
-            auto& s = ctx->prof[L.name];
+            const std::string nm = kernel_name(L);
+            auto& s = ctx->prof[nm];
             s.first += ms;
             s.second += L.flop;
-            ctx->prof_n[L.name] += 1;
+            ctx->prof_n[nm] += 1;
             hipEventDestroy(a);
             hipEventDestroy(b);
         }

@@ -1,0 +1,94 @@
+// avc_bench: native driver of libavc for rocprofv3 runs (no Python in the
+// profiled process).  Same workload as bench.py: full AdaIN-VC SpeakerEncoder
+// config, B utterances x 80 x T frames, n_iters Adam steps, eps 0.1.
+// Weights/inputs are synthetic (uniform / normal from a fixed-seed generator):
+// kernel durations do not depend on the values.
+//
+//   avc_bench [B=256] [T=128] [n_iters=1500] [steps=1] [warmup=0]
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../../include/avc.h"
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        if ((x) != 0) {                                                            \
+            fprintf(stderr, "%s failed: %s\n", #x, avc_last_error());              \
+            return 1;                                                              \
+        }                                                                          \
+    } while (0)
+#define HK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e_));         \
+            return 1;                                                              \
+        }                                                                          \
+    } while (0)
+
+int main(int argc, char** argv) {
+    const int B = argc > 1 ? atoi(argv[1]) : 256;
+    const int T = argc > 2 ? atoi(argv[2]) : 128;
+    const int n_iters = argc > 3 ? atoi(argv[3]) : 1500;
+    const int steps = argc > 4 ? atoi(argv[4]) : 1;
+    const int warmup = argc > 5 ? atoi(argv[5]) : 0;
+
+    avc_se_cfg cfg{};
+    cfg.c_in = 80;
+    cfg.c_h = 128;
+    cfg.c_out = 128;
+    cfg.kernel_size = 5;
+    cfg.bank_size = 8;
+    cfg.bank_scale = 1;
+    cfg.c_bank = 128;
+    cfg.n_conv_blocks = 6;
+    cfg.n_dense_blocks = 6;
+    const int sub[6] = {1, 2, 1, 2, 1, 2};
+    for (int i = 0; i < 6; ++i) cfg.subsample[i] = sub[i];
+    cfg.act = 0;
+
+    const size_t nw = avc_se_weight_count(&cfg);
+    std::mt19937 rng(0);
+    std::uniform_real_distribution<float> uw(-0.05f, 0.05f);
+    std::vector<float> w(nw);
+    for (auto& v : w) v = uw(rng);
+    avc_ctx* ctx = nullptr;
+    CK(avc_create(0, &cfg, w.data(), nw, &ctx));
+
+    const size_t X = (size_t)B * cfg.c_in * T;
+    std::normal_distribution<float> nd(0.f, 1.f);
+    std::vector<float> h(3 * X);
+    for (auto& v : h) v = nd(rng);
+    float *vc, *at, *p0, *out;
+    HK(hipMalloc(&vc, X * 4));
+    HK(hipMalloc(&at, X * 4));
+    HK(hipMalloc(&p0, X * 4));
+    HK(hipMalloc(&out, X * 4));
+    HK(hipMemcpy(vc, h.data(), X * 4, hipMemcpyHostToDevice));
+    HK(hipMemcpy(at, h.data() + X, X * 4, hipMemcpyHostToDevice));
+    HK(hipMemcpy(p0, h.data() + 2 * X, X * 4, hipMemcpyHostToDevice));
+
+    avc_attack_opts o{};
+    o.use_graph = 1;
+    for (int i = 0; i < warmup; ++i) CK(avc_emb_attack(ctx, vc, at, p0, B, T, 0.1f, n_iters, out, &o, nullptr));
+    HK(hipDeviceSynchronize());
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < steps; ++i) CK(avc_emb_attack(ctx, vc, at, p0, B, T, 0.1f, n_iters, out, &o, nullptr));
+    HK(hipDeviceSynchronize());
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<float> res(X);
+    HK(hipMemcpy(res.data(), out, X * 4, hipMemcpyDeviceToHost));
+    double cs = 0;
+    for (float v : res) cs += v;
+    printf("{\"B\": %d, \"T\": %d, \"n_iters\": %d, \"steps\": %d, \"s\": %.4f, \"utts_per_s\": %.3f, "
+           "\"ms_per_iter\": %.4f, \"checksum\": %.6f}\n",
+           B, T, n_iters, steps, s, B * steps / s, s * 1e3 / (steps * (double)n_iters), cs);
+    avc_destroy(ctx);
+    return 0;
+}

@@ -7,33 +7,35 @@
 
 namespace avc {
 
-constexpr int KC = 16;          // K rows staged per chunk (fp32 path)
+constexpr int KSEG = 32;        // K-segment granule: a segment's rows are padded to it, so no K chunk
+                                // (16 or 32 rows) ever straddles two segments
+constexpr int KALIGN = 32;      // A matrices carry zero rows up to a multiple of the largest K chunk
 constexpr int MAX_SEGS = 8;
 
 // How the im2col B-operand rows of one K segment are gathered from HBM.
 enum SegMode : int32_t {
     SEG_FWD = 0,   // x_pad[c][t*stride + j] with reflect padding (models.py:10-30)
-    SEG_BWD = 1,   // adjoint: zero-dilated dY, flipped taps, reflect-pad fold
+    SEG_BWD = 1,   // adjoint: zero-dilated dY, flipped taps, reflect-pad fold (dY already
+                   // gated by ReLU' by its producer)
 };
 
 struct Seg {
     const float* src;    // [B][src_C][src_T]
-    const float* mask;   // BWD: activation whose sign gates dY (act'), or null
-    int32_t k0;          // first K row of the segment (multiple of KC)
-    int32_t kpad;        // rows (C*ks rounded up to KC)
+    int32_t k0;          // first K row of the segment (multiple of KSEG)
+    int32_t kpad;        // rows (C*ks rounded up to KSEG)
     int32_t C;           // channels gathered
     int32_t c_off;       // first channel inside src
     int32_t src_C, src_T;
     int32_t ks, stride, pl, pr;
     int32_t mode;
-    int32_t pad_;
+    int32_t pad_[3];
 };
 
 enum Epi : int32_t {
     EPI_ACT = 0,       // out0 = act(acc + bias)
     EPI_BLOCK = 1,     // a2 = act(acc + bias) -> out0 ; out1 = a2 + avgpool_s(aux0)
     EPI_MASK = 2,      // out0 = acc * act'(aux0)
-    EPI_POOLT = 3,     // out0 = acc + avgpool_s^T(aux0)
+    EPI_POOLT = 3,     // g = acc + avgpool_s^T(aux0); out0 = g (if set); out1 = g*act'(aux1) (if set)
     EPI_INCONV_T = 4,  // rows < split: out0 = acc*act'(aux0) ; rows >= split: out1 = acc
     EPI_ADAM = 5,      // g = acc + aux0 ; tanh backward ; Adam ; adv = vc + eps*tanh(p)
 };
@@ -52,7 +54,7 @@ struct AdamArgs {
 };
 
 struct Problem {
-    int32_t M, Mpad, N, K;     // GEMM: C[M][N] = A[M][K] * B[K][N], K padded
+    int32_t M, Mpad, N, K;     // GEMM: C[M][N] = A[M][K] * B[K][N]; K = end of the last segment
     int32_t T_out;             // columns per utterance (N = B*T_out)
     int32_t nseg;
     int32_t epi, act;
@@ -61,10 +63,14 @@ struct Problem {
     float* out0; int32_t out0_C, out0_coff;
     float* out1; int32_t out1_C, split;
     const float* aux0; int32_t aux0_C, aux0_T;
+    const float* aux1;         // EPI_POOLT: ReLU'-mask source of the masked output out1
     int32_t pool_s;
+    int32_t both_edges;        // BWD gather: T_out <= pl+pr+1, a column may fold from both ends
     int32_t* tick;             // if set, block (0,0) thread 0 increments it (Adam step counter)
     const int32_t* step;       // Adam step counter (read by EPI_ADAM)
     const float* scal;         // per-call scalars: [0] = attack eps, [1] = loss-grad scale
+    int32_t table_len;         // Adam table entries (step is clamped into [1, table_len])
+    int32_t pad2_;
     AdamArgs adam;
     Seg seg[MAX_SEGS];
 };
@@ -75,6 +81,8 @@ struct Problem {
 struct HeadArgs {
     const float* hN;          // [B][C][TN]
     float* g_hN;              // [B][C][TN]   (attack mode)
+    float* g_hN_masked;       // [B][C][TN]   g_hN * act'(mask_hN): the next dgrad's dY
+    const float* mask_hN;     // [B][C][TN]
     const float* Wp;          // packed A fragments, forward
     const float* WpT;         // packed A fragments, backward (transposed)
     const float* bias;        // concatenated biases: dense(2*nd)*C, output D
@@ -84,6 +92,7 @@ struct HeadArgs {
     float* losses;            // [n_iters][B] or null
     const int32_t* step;      // 1-based iteration counter (attack mode)
     const float* scal;        // [1] = 2 / n_elems of the MSE mean (per call)
+    int32_t loss_len;         // rows of `losses` (iterations); writes beyond are dropped
     int32_t B, C, TN, D, n_dense, act, mode;
 };
 

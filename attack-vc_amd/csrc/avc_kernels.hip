@@ -35,47 +35,28 @@ __device__ __forceinline__ float act_d(float y, int act) {
     return y > 0.f ? 1.f : (act ? 0.01f : 0.f);
 }
 
-// Forward im2col element: x_pad[c][t*stride + j] of F.pad(mode="reflect")
-// (models.py:23-29).  Reflect index: -q on the left, 2(T-1)-q on the right.
-__device__ __forceinline__ float gather_fwd(const Seg& S, int b, int t, int c, int j) {
-    int q = t * S.stride + j - S.pl;
-    q = q < 0 ? -q : q;
-    q = q >= S.src_T ? 2 * S.src_T - 2 - q : q;
-    return S.src[((size_t)b * S.src_C + S.c_off + c) * S.src_T + q];
-}
+// Global-address-space views: pointers read out of the Problem table are generic,
+// which would make every gather a flat_load (counted on lgkmcnt as well).
+typedef const float __attribute__((address_space(1)))* gcptr;
+__device__ __forceinline__ gcptr as_global(const float* p) { return (gcptr)p; }
 
-// dY at padded-output coordinate q of a stride-s conv, zero where the
-// dilation leaves holes or outside [0, T_out); optionally gated by act'(mask).
-__device__ __forceinline__ float dy_at(const float* __restrict__ row, const float* __restrict__ mrow,
-                                       int q, int stride, int T, int act) {
-    if (q < 0) return 0.f;
+// Index of dY for padded-output coordinate q of a stride-s conv; `ok` is false
+// where the zero-dilation leaves a hole or q falls outside [0, T).  The caller
+// loads row[idx] unconditionally (idx is clamped in range) and selects later, so
+// no load waits inside the gather loop.  STRIDE = 0: runtime stride `rs`.
+template <int STRIDE>
+__device__ __forceinline__ int dy_index(int q, int rs, int T, bool& ok) {
     int qq = q;
-    if (stride == 2) {
-        if (q & 1) return 0.f;
+    ok = q >= 0;
+    if (STRIDE == 2) {
+        ok = ok && !(q & 1);
         qq = q >> 1;
-    } else if (stride != 1) {
-        qq = q / stride;
-        if (qq * stride != q) return 0.f;
+    } else if (STRIDE == 0 && rs != 1) {
+        qq = q / rs;
+        ok = ok && qq * rs == q;
     }
-    if (qq >= T) return 0.f;
-    float v = row[qq];
-    if (mrow) v *= act_d(mrow[qq], act);
-    return v;
-}
-
-// Adjoint im2col element for the input gradient of a reflect-padded conv:
-//   dX[c][t] = sum_{co,j} W[co][c][j] * sum_{p in pad^-1(t)} dY[co][(p - j)/s]
-// pad^-1(t) = {t + pl} u {pl - t if 1<=t<=pl} u {pl + 2T - 2 - t if T-1-pr<=t<=T-2}.
-// (K row = (co, j); t is the dgrad output position, T its length.)
-__device__ __forceinline__ float gather_bwd(const Seg& S, int b, int t, int c, int j, int T, int act) {
-    const size_t off = ((size_t)b * S.src_C + S.c_off + c) * S.src_T;
-    const float* row = S.src + off;
-    const float* mrow = S.mask ? S.mask + off : nullptr;
-    float v = dy_at(row, mrow, t + S.pl - j, S.stride, S.src_T, act);
-    if (t >= 1 && t <= S.pl) v += dy_at(row, mrow, S.pl - t - j, S.stride, S.src_T, act);
-    if (t >= T - 1 - S.pr && t <= T - 2)
-        v += dy_at(row, mrow, S.pl + 2 * T - 2 - t - j, S.stride, S.src_T, act);
-    return v;
+    ok = ok && qq < T;
+    return ok ? qq : 0;
 }
 
 __device__ __forceinline__ void epilogue(const Problem& P, int m, int b, int t, float acc) {
@@ -118,7 +99,11 @@ __device__ __forceinline__ void epilogue(const Problem& P, int m, int b, int t, 
         } else {
             r = g[t];
         }
-        P.out0[((size_t)b * P.out0_C + m) * T + t] = acc + r;
+        const float gv = acc + r;
+        const size_t o = ((size_t)b * P.out0_C + m) * T + t;
+        if (P.out0) P.out0[o] = gv;
+        // masked copy = the next dgrad's dY (ReLU' of the forward activation aux1)
+        if (P.out1) P.out1[o] = gv * act_d(P.aux1[o], P.act);
         break;
     }
     case EPI_INCONV_T: {  // split d(cat)/d: bank part gated by its ReLU, x part passes through
@@ -141,7 +126,7 @@ __device__ __forceinline__ void epilogue(const Problem& P, int m, int b, int t, 
         const float th = tanhf(p);
         const float eps = P.scal[0];
         const float g = (gadv * eps) * (1.f - th * th);
-        const int step = *P.step;
+        const int step = min(max(*P.step, 1), P.table_len);
         if (A.grad0 && step == 1) A.grad0[idx] = g;
         float mm = A.m[idx];
         mm = mm + A.b1c * (g - mm);
@@ -162,7 +147,7 @@ __device__ __forceinline__ void epilogue(const Problem& P, int m, int b, int t, 
     }
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int KC, int MODE, int STRIDE>
 __global__ void __launch_bounds__(256) conv_gemm_f32(const Problem* __restrict__ probs) {
     constexpr int MT = 64 * WM, NT = 64 * WN;
     const Problem& P = probs[blockIdx.z];
@@ -179,20 +164,27 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const Problem* __restrict__
     const int wm = wave >> 1, wn = wave & 1;
     const int r32 = lane & 31, h = lane >> 5;
 
-    // B loader: lanes <-> columns n, waves <-> K rows (so (c, j) is wave-uniform)
+    const int N = P.N, T_out = P.T_out, Kend = P.K, Mpad = P.Mpad, nseg = P.nseg, act = P.act;
+    const float* __restrict__ At = P.At;
+
+    // B loader: lanes <-> columns n; each thread owns BPASS consecutive K rows of the
+    // chunk, so (segment, c, j) is wave-uniform and advances by one tap per row.
     constexpr int BROWS = 256 / NT;
     constexpr int BPASS = KC / BROWS;
     const int nl = tid % NT;
-    const int kr0 = __builtin_amdgcn_readfirstlane(tid / NT);
+    const int rg = __builtin_amdgcn_readfirstlane(tid / NT);
     const int n = n0 + nl;
-    const bool nvalid = n < P.N;
-    const int T_out = P.T_out;
+    const bool nvalid = n < N;
     const int bb = nvalid ? n / T_out : 0;
     const int tt = nvalid ? n - bb * T_out : 0;
 
     constexpr int AF4 = KC * MT / 4 / 256;
+    static_assert(BPASS <= 16, "validity mask packs 16 rows");
     f32x4 areg[AF4];
     float breg[BPASS];
+    float ereg[MODE == SEG_BWD ? BPASS : 1];   // reflect-fold term of the adjoint gather
+    unsigned vmask = 0u;                       // bit p: main term valid; bit 16+p: fold term valid
+    const bool both_edges = MODE == SEG_BWD && P.both_edges;
 
     f32x16 acc[WM][WN];
 #pragma unroll
@@ -202,26 +194,65 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const Problem* __restrict__
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    const gcptr gAt = as_global(At);
     auto load_chunk = [&](int kc) {
         const int k0 = kc * KC;
-        int si = 0;
-        while (si + 1 < P.nseg && k0 >= P.seg[si + 1].k0) ++si;
-        const Seg& S = P.seg[si];
 #pragma unroll
         for (int i = 0; i < AF4; ++i) {
             const int f = tid + i * 256;
             const int r = f / (MT / 4), c4 = f % (MT / 4);
-            areg[i] = *reinterpret_cast<const f32x4*>(P.At + (size_t)(k0 + r) * P.Mpad + m0 + 4 * c4);
+            areg[i] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
+                gAt + (size_t)(k0 + r) * Mpad + m0 + 4 * c4);
         }
+        // chunks never straddle segments (segments are padded to KSEG rows)
+        int si = 0;
+        while (si + 1 < nseg && k0 >= P.seg[si + 1].k0) ++si;
+        const Seg& S = P.seg[si];
+        const int ks = S.ks, pl = S.pl, srcT = S.src_T, C = S.C;
+        const gcptr base = as_global(S.src) + ((size_t)bb * S.src_C + S.c_off) * srcT;
+        const int kk0 = k0 - S.k0 + rg * BPASS;
+        int c = kk0 / ks;
+        int j = kk0 - c * ks;
+        vmask = 0u;
 #pragma unroll
         for (int p = 0; p < BPASS; ++p) {
-            const int kk = k0 + kr0 + p * BROWS - S.k0;
-            const int c = kk / S.ks;
-            const int j = kk - c * S.ks;
-            float v = 0.f;
-            if (nvalid && c < S.C)
-                v = (S.mode == SEG_FWD) ? gather_fwd(S, bb, tt, c, j) : gather_bwd(S, bb, tt, c, j, T_out, P.act);
-            breg[p] = v;
+            const bool live = c < C;                        // wave-uniform (padded rows are 0)
+            const gcptr row = base + (size_t)(live ? c : 0) * srcT;
+            if (MODE == SEG_FWD) {
+                // x_pad[c][t*stride + j] of F.pad(mode="reflect") (models.py:23-29)
+                const int st = STRIDE ? STRIDE : S.stride;
+                int q = tt * st + j - pl;
+                q = q < 0 ? -q : q;
+                q = q >= srcT ? 2 * srcT - 2 - q : q;
+                breg[p] = row[q];
+                vmask |= (live ? 1u : 0u) << p;
+            } else {
+                // adjoint: dX[c][t] = sum_{co,j} W[co][c][j] sum_{p in pad^-1(t)} dY[co][(p-j)/s]
+                // pad^-1(t) = {t+pl} u {pl-t : 1<=t<=pl} u {pl+2T-2-t : T-1-pr<=t<=T-2}
+                const int rs = S.stride, pr = S.pr;
+                bool ok0, ok1;
+                const int i0 = dy_index<STRIDE>(tt + pl - j, rs, srcT, ok0);
+                const bool left = tt >= 1 && tt <= pl;
+                const bool right = tt >= T_out - 1 - pr && tt <= T_out - 2;
+                // one fold term per lane (the left one if a tiny T_out <= pl+pr+1 gives both)
+                const int qe = left ? pl - tt - j : (right ? pl + 2 * T_out - 2 - tt - j : -1);
+                const int i1 = dy_index<STRIDE>(qe, rs, srcT, ok1);
+                breg[p] = row[i0];
+                ereg[p] = row[i1];
+                if (both_edges) {   // tiny T only: here a waited load is acceptable
+                    bool ok2;
+                    const int i2 = dy_index<STRIDE>(left && right ? pl + 2 * T_out - 2 - tt - j : -1, rs, srcT, ok2);
+                    const float e2 = row[i2];
+                    ereg[p] = (ok1 ? ereg[p] : 0.f) + (ok2 ? e2 : 0.f);
+                    ok1 = true;
+                }
+                vmask |= ((live && ok0) ? 1u : 0u) << p;
+                vmask |= ((live && ok1) ? 1u : 0u) << (16 + p);
+            }
+            if (++j == ks) {
+                j = 0;
+                ++c;
+            }
         }
     };
     auto store_chunk = [&]() {
@@ -232,10 +263,14 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const Problem* __restrict__
             *reinterpret_cast<f32x4*>(&ldsA[r * MT + 4 * c4]) = areg[i];
         }
 #pragma unroll
-        for (int p = 0; p < BPASS; ++p) ldsB[(kr0 + p * BROWS) * NT + nl] = breg[p];
+        for (int p = 0; p < BPASS; ++p) {
+            float v = ((vmask >> p) & 1u) ? breg[p] : 0.f;
+            if (MODE == SEG_BWD) v += ((vmask >> (16 + p)) & 1u) ? ereg[p] : 0.f;
+            ldsB[(rg * BPASS + p) * NT + nl] = nvalid ? v : 0.f;
+        }
     };
 
-    const int nchunks = P.K / KC;
+    const int nchunks = (Kend + KC - 1) / KC;
     load_chunk(0);
     for (int kc = 0; kc < nchunks; ++kc) {
         __syncthreads();
@@ -284,9 +319,19 @@ __global__ void __launch_bounds__(256) conv_gemm_f32(const Problem* __restrict__
     }
 }
 
-template __global__ void conv_gemm_f32<2, 2>(const Problem*);
-template __global__ void conv_gemm_f32<2, 1>(const Problem*);
-template __global__ void conv_gemm_f32<1, 1>(const Problem*);
+#define AVC_INST_T(WM, WN, KC)                                                     \
+    template __global__ void conv_gemm_f32<WM, WN, KC, SEG_FWD, 1>(const Problem*); \
+    template __global__ void conv_gemm_f32<WM, WN, KC, SEG_FWD, 2>(const Problem*); \
+    template __global__ void conv_gemm_f32<WM, WN, KC, SEG_FWD, 0>(const Problem*); \
+    template __global__ void conv_gemm_f32<WM, WN, KC, SEG_BWD, 1>(const Problem*); \
+    template __global__ void conv_gemm_f32<WM, WN, KC, SEG_BWD, 2>(const Problem*); \
+    template __global__ void conv_gemm_f32<WM, WN, KC, SEG_BWD, 0>(const Problem*);
+AVC_INST_T(2, 2, 32)
+AVC_INST_T(2, 2, 16)
+AVC_INST_T(2, 1, 32)
+AVC_INST_T(1, 1, 32)
+AVC_INST_T(1, 1, 16)
+#undef AVC_INST_T
 
 // ---------------------------------------------------------------------------------
 // se_head
@@ -301,16 +346,20 @@ __device__ __forceinline__ void head_gemm(const float* __restrict__ Wpk, int M, 
                                           int act, bool apply_act, int wave, int lane) {
     if (wave * 16 >= M) return;
     const float* Wt = Wpk + (size_t)wave * (K / 4) * 64;
+    // all of this wave's A fragments in flight at once (K <= 128 -> <= 32 per lane)
+    float a[32];
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) a[kk] = (4 * kk < K) ? Wt[kk * 64 + lane] : 0.f;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     const int hh = lane >> 4, col = lane & 15;
-#pragma unroll 2
-    for (int kk = 0; kk < K / 4; kk += 2) {
-        const float a0 = Wt[kk * 64 + lane];
-        const float a1 = Wt[(kk + 1) * 64 + lane];
-        const float b0 = X[(4 * kk + hh) * HU + col];
-        const float b1 = X[(4 * kk + 4 + hh) * HU + col];
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc1, 0, 0, 0);
+#pragma unroll
+    for (int kk = 0; kk < 32; kk += 2) {
+        if (4 * kk < K) {
+            const float b0 = X[(4 * kk + hh) * HU + col];
+            const float b1 = X[(4 * kk + 4 + hh) * HU + col];
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk + 1], b1, acc1, 0, 0, 0);
+        }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -380,7 +429,7 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
     const int step = *A.step;
     if (tid < HU) {
         const int b = u0 + tid;
-        if (b < A.B && A.losses) {
+        if (b < A.B && A.losses && step >= 1 && step <= A.loss_len) {
             float s1 = 0.f, s2 = 0.f;
             for (int d = 0; d < D; ++d) {
                 const float e = EMB[d * HU + tid];
@@ -425,12 +474,14 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
     }
     // d/d hN of the mean over time
     const int TN = A.TN;
-    for (int idx = tid; idx < C * HU * TN; idx += blockDim.x) {
-        const int t = idx % TN;
-        const int rest = idx / TN;
-        const int c = rest % C, u = rest / C;
-        const int b = u0 + u;
-        if (b < A.B) A.g_hN[((size_t)b * C + c) * TN + t] = GB[c * HU + u] / (float)TN;
+    for (int u = 0; u < HU && u0 + u < A.B; ++u) {
+        const size_t off = (size_t)(u0 + u) * C * TN;
+        for (int idx = tid; idx < C * TN; idx += blockDim.x) {
+            const int c = idx / TN;
+            const float g = GB[c * HU + u] / (float)TN;
+            A.g_hN[off + idx] = g;
+            A.g_hN_masked[off + idx] = g * act_d(A.mask_hN[off + idx], A.act);
+        }
     }
 }
 
