@@ -16,8 +16,8 @@
 #include "avc_kernels.h"
 
 namespace avc {
-template <int WM, int WN, int KC, int MODE, int STRIDE>
-__global__ void conv_gemm_f32(const Problem* __restrict__ probs);
+template <int PREC, int WM, int WN, int WGM, int WGN, int KC, int MODE, int STRIDE>
+__global__ void conv_gemm(const Problem* __restrict__ probs);
 __global__ void se_head(HeadArgs A);
 __global__ void attack_init(const float* vc, const float* ptb0, float* ptb, float* m, float* v, float* adv,
                             float eps, size_t n);
@@ -63,22 +63,26 @@ struct HostConv {
 
 enum LaunchKind { L_GEMM, L_HEAD };
 
-// conv_gemm_f32 instantiations (tile = 64*WM x 64*WN, K chunk KC); the planner
-// autotunes one per launch on first use of a workspace.
+// conv_gemm instantiations (avc_gemm_variants.h); the planner autotunes one per
+// launch and precision on first use of a workspace.
 struct Variant {
-    int wm, wn, kc;
+    int prec, wm, wn, wgm, wgn, kc;
     const char* name;
+    int mt() const { return 32 * wm * wgm; }
+    int nt() const { return 32 * wn * wgn; }
+    int threads() const { return 64 * wgm * wgn; }
 };
 static const Variant VARIANTS[] = {
-    {2, 2, 32, "conv_gemm_f32<128x128,k32>"}, {2, 2, 16, "conv_gemm_f32<128x128,k16>"},
-    {2, 1, 32, "conv_gemm_f32<128x64,k32>"},  {1, 1, 32, "conv_gemm_f32<64x64,k32>"},
-    {1, 1, 16, "conv_gemm_f32<64x64,k16>"},
+#define AVC_GEMM_VARIANT(I, PREC, WM, WN, WGM, WGN, KC, NAME) {PREC, WM, WN, WGM, WGN, KC, NAME},
+#include "avc_gemm_variants.h"
+#undef AVC_GEMM_VARIANT
 };
 constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
 struct Launch {
     int kind;
     int variant = 0;             // L_GEMM: index into VARIANTS
+    int prec = PREC_F32;         // L_GEMM: operand precision of the MFMAs
     int mode = 0, stride = 1;    // L_GEMM: loader specialisation shared by all its problems
     int maxM = 0, maxN = 0;      // L_GEMM: grid extents over its problems
     dim3 grid, block;
@@ -103,8 +107,8 @@ struct Workspace {
     DevBuf losses, table, scal;
     int iters_cap = 0;
     int* step = nullptr;
-    Plan fwd, iter;
-    hipGraphExec_t graph = nullptr;
+    Plan fwd, iter, iter_bf16;
+    hipGraphExec_t graph = nullptr, graph_bf16 = nullptr;
     bool built = false;
 };
 
@@ -125,6 +129,7 @@ struct avc_ctx {
     DevBuf bias_in;
     std::vector<DevBuf> bias_c1, bias_c2;
     DevBuf head_Wp, head_WpT, head_bias;
+    std::map<const float*, void*> bf16_of;   // fp32 A matrix -> its bf16 copy (device)
     hipStream_t stream = nullptr;
     hipEvent_t ev_user = nullptr, ev_done = nullptr;
     Workspace ws;
@@ -153,17 +158,41 @@ static void dfree(DevBuf& b) {
     b.n = 0;
 }
 
-// A matrices ([K][Mpad]) get zero rows up to a multiple of KALIGN so every K chunk
-// size the kernels use reads in bounds.
-static std::vector<float> pad_rows(std::vector<float> At, int Mpad) {
-    const size_t rows = At.size() / Mpad;
-    At.resize((size_t)rup((int)rows, KALIGN) * Mpad, 0.f);
-    return At;
+// The packers build A^T as [K][Mpad]; the kernels read A row-major [Mpad][Kld]
+// (k contiguous, Kld = K rounded up to KALIGN with zero columns) so that a K
+// chunk of one output row is one 16-byte-vectorised run in HBM and in LDS.
+static std::vector<float> pad_rows(const std::vector<float>& At, int Mpad) {
+    const int K = (int)(At.size() / Mpad);
+    const int Kld = rup(K, KALIGN);
+    std::vector<float> A((size_t)Mpad * Kld, 0.f);
+    for (int k = 0; k < K; ++k)
+        for (int m = 0; m < Mpad; ++m) A[(size_t)m * Kld + k] = At[(size_t)k * Mpad + m];
+    return A;
 }
 
 static int upload(DevBuf& b, const std::vector<float>& h) {
     if (dalloc(b, h.size())) return 1;
     HIPCHK(hipMemcpy(b.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// fp32 -> bf16, round to nearest even (weights: finite values)
+static uint16_t to_bf16(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+// upload an A matrix in fp32 and in bf16 (the bf16 path's MFMA operand)
+static int upload_A(avc_ctx* ctx, DevBuf& b, const std::vector<float>& h) {
+    if (upload(b, h)) return 1;
+    std::vector<uint16_t> hb(h.size());
+    for (size_t i = 0; i < h.size(); ++i) hb[i] = to_bf16(h[i]);
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, hb.size() * 2));
+    HIPCHK(hipMemcpy(d, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+    ctx->bf16_of[b.p] = d;
     return 0;
 }
 
@@ -302,6 +331,7 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
 
     int rc = 0;
     auto up = [&](DevBuf& b, const std::vector<float>& h) { rc |= upload(b, h); };
+    auto upA = [&](DevBuf& b, const std::vector<float>& h) { rc |= upload_A(ctx, b, h); };
     auto upv = [&](DevBuf& b, const float* src, size_t n) { up(b, std::vector<float>(src, src + n)); };
 
     // ---- forward packs
@@ -309,7 +339,7 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
     ctx->AtF_bank.resize(nb);
     ctx->bias_bank.resize(nb);
     for (int i = 0; i < nb; ++i) {
-        up(ctx->AtF_bank[i], pad_rows(pack_fwd(bank[i], MpadB), MpadB));
+        upA(ctx->AtF_bank[i], pad_rows(pack_fwd(bank[i], MpadB), MpadB));
         upv(ctx->bias_bank[i], bank[i].b, c.c_bank);
     }
     {
@@ -318,13 +348,13 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
         std::vector<float> At((size_t)(k1 + k2) * MpadH, 0.f);
         pack_fwd(inc, MpadH, 0, k1 + k2, &At, 0, c.c_bank * nb);
         pack_fwd(inc, MpadH, k1, k1 + k2, &At, c.c_bank * nb, c.c_in);
-        up(ctx->AtF_in, pad_rows(At, MpadH));
+        upA(ctx->AtF_in, pad_rows(At, MpadH));
         upv(ctx->bias_in, inc.b, c.c_h);
         // in_conv dgrad: M = cin_cat rows (ci), K = c_h (co): At[co][ci] = W[co][ci]
         const int MpadI = rup(cin_cat, 128);
         std::vector<float> Bt((size_t)rup(c.c_h, KSEG) * MpadI, 0.f);
         pack_bwd(inc, MpadI, 0, Bt);
-        up(ctx->AtB_in, pad_rows(Bt, MpadI));
+        upA(ctx->AtB_in, pad_rows(Bt, MpadI));
     }
     ctx->AtF_c1.resize(c.n_conv_blocks);
     ctx->AtF_c2.resize(c.n_conv_blocks);
@@ -334,14 +364,14 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
     ctx->bias_c2.resize(c.n_conv_blocks);
     for (int l = 0; l < c.n_conv_blocks; ++l) {
         const int MpadH = rup(c.c_h, 128);
-        up(ctx->AtF_c1[l], pad_rows(pack_fwd(c1[l], MpadH), MpadH));
-        up(ctx->AtF_c2[l], pad_rows(pack_fwd(c2[l], MpadH), MpadH));
+        upA(ctx->AtF_c1[l], pad_rows(pack_fwd(c1[l], MpadH), MpadH));
+        upA(ctx->AtF_c2[l], pad_rows(pack_fwd(c2[l], MpadH), MpadH));
         const int Kb = rup(c.c_h * c.kernel_size, KSEG);
         std::vector<float> b1((size_t)Kb * MpadH, 0.f), b2((size_t)Kb * MpadH, 0.f);
         pack_bwd(c1[l], MpadH, 0, b1);
         pack_bwd(c2[l], MpadH, 0, b2);
-        up(ctx->AtB_c1[l], pad_rows(b1, MpadH));
-        up(ctx->AtB_c2[l], pad_rows(b2, MpadH));
+        upA(ctx->AtB_c1[l], pad_rows(b1, MpadH));
+        upA(ctx->AtB_c2[l], pad_rows(b2, MpadH));
         upv(ctx->bias_c1[l], c1[l].b, c.c_h);
         upv(ctx->bias_c2[l], c2[l].b, c.c_h);
     }
@@ -358,7 +388,7 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
             pack_bwd(bank[i], MpadX, row, At);
             row += ctx->kpadB_bank[i];
         }
-        up(ctx->AtB_bank, pad_rows(At, MpadX));
+        upA(ctx->AtB_bank, pad_rows(At, MpadX));
     }
     {   // head
         const size_t CC = (size_t)c.c_h * c.c_h;
@@ -402,11 +432,17 @@ static void free_plan(Plan& pl) {
     pl.launches.clear();
 }
 
-static void free_ws(Workspace& ws) {
-    if (ws.graph) hipGraphExecDestroy(ws.graph);
-    ws.graph = nullptr;
+static void free_plans(Workspace& ws) {
+    if (ws.graph) (void)hipGraphExecDestroy(ws.graph);
+    if (ws.graph_bf16) (void)hipGraphExecDestroy(ws.graph_bf16);
+    ws.graph = ws.graph_bf16 = nullptr;
     free_plan(ws.fwd);
     free_plan(ws.iter);
+    free_plan(ws.iter_bf16);
+}
+
+static void free_ws(Workspace& ws) {
+    free_plans(ws);
     DevBuf* bufs[] = {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.bank, &ws.h0, &ws.gbank, &ws.gxd,
                       &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal};
     for (DevBuf* b : bufs) dfree(*b);
@@ -434,6 +470,8 @@ extern "C" void avc_destroy(avc_ctx* ctx) {
     for (DevBuf* b : {&ctx->AtF_in, &ctx->AtB_in, &ctx->AtB_bank, &ctx->bias_in, &ctx->head_Wp,
                       &ctx->head_WpT, &ctx->head_bias})
         dfree(*b);
+    for (auto& kv : ctx->bf16_of) (void)hipFree(kv.second);
+    ctx->bf16_of.clear();
     if (ctx->ev_user) hipEventDestroy(ctx->ev_user);
     if (ctx->ev_done) hipEventDestroy(ctx->ev_done);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -477,33 +515,49 @@ static Problem base_problem(int M, int Mpad, int N, int T_out, const float* At, 
 static void add_seg(Problem& p, const Seg& s) {
     p.seg[p.nseg++] = s;
     p.K = s.k0 + s.kpad;
+    p.Kld = rup(p.K, KALIGN);
 }
 
-static dim3 gemm_grid(const Launch& L) {
-    const Variant& v = VARIANTS[L.variant];
-    return dim3(cdiv(L.maxN, 64 * v.wn), cdiv(L.maxM, 64 * v.wm), L.nprob);
+static dim3 gemm_grid(const Launch& L, int variant) {
+    const Variant& v = VARIANTS[variant];
+    return dim3(cdiv(L.maxN, v.nt()), cdiv(L.maxM, v.mt()), L.nprob);
 }
 
-// default tile before autotuning: enough workgroups to fill 256 CUs
-static int default_variant(const std::vector<Problem>& ps) {
-    auto count = [&](int MT, int NT) {
-        long n = 0;
-        for (auto& p : ps) n += (long)cdiv(p.M, MT) * cdiv(p.N, NT);
-        return n;
-    };
-    if (count(128, 128) >= 512) return 0;
-    if (count(128, 64) >= 512) return 2;
-    return 3;
+// default tile before autotuning: the largest tile of this precision whose grid
+// still has >= 512 workgroups (2 per CU), else the smallest tile
+static int default_variant(const std::vector<Problem>& ps, int prec) {
+    int best = -1, small = -1;
+    long best_area = 0, small_area = 1L << 40;
+    for (int v = 0; v < NVARIANTS; ++v) {
+        if (VARIANTS[v].prec != prec) continue;
+        const long area = (long)VARIANTS[v].mt() * VARIANTS[v].nt();
+        long wgs = 0;
+        for (auto& p : ps) wgs += (long)cdiv(p.M, VARIANTS[v].mt()) * cdiv(p.N, VARIANTS[v].nt());
+        if (wgs >= 512 && area > best_area) {
+            best = v;
+            best_area = area;
+        }
+        if (area < small_area) {
+            small = v;
+            small_area = area;
+        }
+    }
+    return best >= 0 ? best : small;
 }
 
-static int add_gemm(Plan& pl, std::vector<Problem> ps, double flop, const char* what) {
+static int add_gemm(avc_ctx* ctx, Plan& pl, std::vector<Problem> ps, double flop, const std::string& what,
+                    int prec) {
     int gx = 0, gy = 0;
     for (auto& p : ps) {
+        auto it = ctx->bf16_of.find(p.At);
+        if (it == ctx->bf16_of.end()) return fail("internal: no bf16 copy of an A matrix");
+        p.Ab = it->second;
         for (int i = 0; i < p.nseg; ++i)
             if (p.seg[i].mode != ps[0].seg[0].mode || p.seg[i].stride != ps[0].seg[0].stride)
                 return fail("internal: mixed loader modes in one launch");
         if (p.K % KSEG) return fail("internal: K %d not a multiple of %d", p.K, KSEG);
         if (p.Mpad % 128) return fail("internal: Mpad %d not a multiple of 128", p.Mpad);
+        if (p.Kld != rup(p.K, KALIGN)) return fail("internal: Kld %d for K %d", p.Kld, p.K);
         gx = std::max(gx, p.N);
         gy = std::max(gy, p.M);
     }
@@ -513,7 +567,8 @@ static int add_gemm(Plan& pl, std::vector<Problem> ps, double flop, const char* 
     pl.owned.push_back(d);
     Launch L;
     L.kind = L_GEMM;
-    L.variant = default_variant(ps);
+    L.prec = prec;
+    L.variant = default_variant(ps, prec);
     L.mode = ps[0].seg[0].mode;
     L.stride = ps[0].seg[0].stride;
     L.maxN = gx;
@@ -528,7 +583,7 @@ static int add_gemm(Plan& pl, std::vector<Problem> ps, double flop, const char* 
 }
 
 // SpeakerEncoder forward (models.py:327-343) from `x` up to h_N, then the head.
-static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, bool attack) {
+static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, bool attack, int prec) {
     const avc_se_cfg& c = ctx->cfg;
     const int B = ws.B, T = ws.T, nb = ctx->nb;
     const int N0 = B * T;
@@ -550,7 +605,7 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
             ps.push_back(p);
             flop += 2.0 * c.c_bank * c.c_in * k * N0;
         }
-        if (add_gemm(pl, ps, flop, "bank")) return 1;
+        if (add_gemm(ctx, pl, ps, flop, "bank", prec)) return 1;
     }
     {   // in_conv_layer over cat(bank, x) (models.py:103,337-338)
         Problem p = base_problem(c.c_h, rup(c.c_h, 128), N0, T, ctx->AtF_in.p, ctx->bias_in.p, c.act);
@@ -559,7 +614,7 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
         p.epi = EPI_ACT;
         p.out0 = ws.h0.p;
         p.out0_C = c.c_h;
-        if (add_gemm(pl, {p}, 2.0 * c.c_h * (nb * c.c_bank + c.c_in) * N0, "in_conv")) return 1;
+        if (add_gemm(ctx, pl, {p}, 2.0 * c.c_h * (nb * c.c_bank + c.c_in) * N0, "in_conv", prec)) return 1;
     }
     int kpl, kpr;
     pads_of(c.kernel_size, kpl, kpr);
@@ -571,7 +626,7 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
         p1.epi = EPI_ACT;
         p1.out0 = ws.a1[l].p;
         p1.out0_C = c.c_h;
-        if (add_gemm(pl, {p1}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * Ti, "conv1")) return 1;
+        if (add_gemm(ctx, pl, {p1}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * Ti, "conv1.b" + std::to_string(l), prec)) return 1;
         Problem p2 = base_problem(c.c_h, rup(c.c_h, 128), B * To, To, ctx->AtF_c2[l].p, ctx->bias_c2[l].p, c.act);
         add_seg(p2, make_seg(ws.a1[l].p, 0, c.c_h, 0, c.c_h, Ti, c.kernel_size, s, kpl, kpr, SEG_FWD));
         p2.epi = EPI_BLOCK;
@@ -583,7 +638,7 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
         p2.aux0_C = c.c_h;
         p2.aux0_T = Ti;
         p2.pool_s = s;
-        if (add_gemm(pl, {p2}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * To, "conv2")) return 1;
+        if (add_gemm(ctx, pl, {p2}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * To, "conv2.b" + std::to_string(l), prec)) return 1;
     }
     {   // head
         Launch L;
@@ -623,7 +678,7 @@ static int plan_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, b
 }
 
 // Input-gradient of the SpeakerEncoder back to the perturbation + Adam (fused).
-static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
+static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) {
     const avc_se_cfg& c = ctx->cfg;
     const int B = ws.B, T = ws.T, nb = ctx->nb;
     int kpl, kpr;
@@ -647,7 +702,7 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
         p2.aux0 = ws.a1[l].p;
         p2.aux0_C = c.c_h;
         p2.aux0_T = Ti;
-        if (add_gemm(pl, {p2}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * To, "conv2_dgrad")) return 1;
+        if (add_gemm(ctx, pl, {p2}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * To, "conv2_dgrad.b" + std::to_string(l), prec)) return 1;
         // conv1^T + residual avg-pool^T -> g(h_l), and its copy masked by the ReLU that
         // produced h_l (a2_{l-1}, or h0's in_conv ReLU for l = 0)
         Problem p1 = base_problem(c.c_h, MpadH, B * Ti, Ti, ctx->AtB_c1[l].p, nullptr, c.act);
@@ -663,7 +718,7 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
         p1.aux0_C = c.c_h;
         p1.aux0_T = To;
         p1.pool_s = s;
-        if (add_gemm(pl, {p1}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * Ti, "conv1_dgrad")) return 1;
+        if (add_gemm(ctx, pl, {p1}, 2.0 * c.c_h * c.c_h * c.kernel_size * B * Ti, "conv1_dgrad.b" + std::to_string(l), prec)) return 1;
         std::swap(gcur, gnext);
         std::swap(mcur, mnext);
     }
@@ -681,7 +736,7 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
         p.aux0 = ws.bank.p;
         p.aux0_C = nb * c.c_bank;
         p.aux0_T = T;
-        if (add_gemm(pl, {p}, 2.0 * c.c_h * cin_cat * N0, "in_conv_dgrad")) return 1;
+        if (add_gemm(ctx, pl, {p}, 2.0 * c.c_h * cin_cat * N0, "in_conv_dgrad", prec)) return 1;
     }
     {   // conv bank^T over all kernels + x passthrough + tanh' + Adam
         Problem p = base_problem(c.c_in, rup(c.c_in, 128), N0, T, ctx->AtB_bank.p, nullptr, c.act);
@@ -715,7 +770,7 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl) {
         A.b2 = 0.999f;
         A.b2c = (float)(1.0 - 0.999);
         A.adam_eps = 1e-8f;
-        if (add_gemm(pl, {p}, flop, "bank_dgrad_adam")) return 1;
+        if (add_gemm(ctx, pl, {p}, flop, "bank_dgrad_adam", prec)) return 1;
     }
     return 0;
 }
@@ -780,14 +835,11 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     if (dalloc(ws.losses, (size_t)cap * B)) return 1;
     if (dalloc(ws.table, (size_t)cap * 2)) return 1;
     ws.iters_cap = cap;
-    // (re)build plans: pointers may have moved
-    if (ws.graph) hipGraphExecDestroy(ws.graph);
-    ws.graph = nullptr;
-    free_plan(ws.fwd);
-    free_plan(ws.iter);
-    if (plan_forward(ctx, ws, ws.fwd, ws.xin.p, false)) return 1;
-    if (plan_forward(ctx, ws, ws.iter, ws.adv.p, true)) return 1;
-    if (plan_backward(ctx, ws, ws.iter)) return 1;
+    // (re)build plans: pointers may have moved (the bf16 plan is rebuilt on demand)
+    free_plans(ws);
+    if (plan_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return 1;
+    if (plan_forward(ctx, ws, ws.iter, ws.adv.p, true, PREC_F32)) return 1;
+    if (plan_backward(ctx, ws, ws.iter, PREC_F32)) return 1;
     // autotune with a valid Adam step (1) and eps/gscale (the kernels clamp anyway)
     const float scal0[4] = {0.1f, 0.f, 0.f, 0.f};
     HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
@@ -797,31 +849,34 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     return 0;
 }
 
-template <int WM, int WN, int KC>
-static void launch_tile(const Launch& L, dim3 g, hipStream_t s) {
+template <int PREC, int WM, int WN, int WGM, int WGN, int KC>
+static void launch_variant(const Launch& L, dim3 g, hipStream_t s) {
+    const dim3 blk(64 * WGM * WGN);
     const int st = (L.stride == 1 || L.stride == 2) ? L.stride : 0;
+#define AVC_L(MODE, ST) hipLaunchKernelGGL((conv_gemm<PREC, WM, WN, WGM, WGN, KC, MODE, ST>), g, blk, 0, s, L.dprobs)
     if (L.mode == SEG_FWD) {
-        if (st == 1) hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_FWD, 1>), g, L.block, 0, s, L.dprobs);
-        else if (st == 2) hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_FWD, 2>), g, L.block, 0, s, L.dprobs);
-        else hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_FWD, 0>), g, L.block, 0, s, L.dprobs);
+        if (st == 1) AVC_L(SEG_FWD, 1);
+        else if (st == 2) AVC_L(SEG_FWD, 2);
+        else AVC_L(SEG_FWD, 0);
     } else {
-        if (st == 1) hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_BWD, 1>), g, L.block, 0, s, L.dprobs);
-        else if (st == 2) hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_BWD, 2>), g, L.block, 0, s, L.dprobs);
-        else hipLaunchKernelGGL((conv_gemm_f32<WM, WN, KC, SEG_BWD, 0>), g, L.block, 0, s, L.dprobs);
+        if (st == 1) AVC_L(SEG_BWD, 1);
+        else if (st == 2) AVC_L(SEG_BWD, 2);
+        else AVC_L(SEG_BWD, 0);
     }
+#undef AVC_L
 }
 
 static hipError_t launch_gemm(const Launch& L, int variant, hipStream_t s) {
-    Launch V = L;
-    V.variant = variant;
-    const dim3 g = gemm_grid(V);
+    const dim3 g = gemm_grid(L, variant);
     switch (variant) {
-    case 0: launch_tile<2, 2, 32>(L, g, s); break;
-    case 1: launch_tile<2, 2, 16>(L, g, s); break;
-    case 2: launch_tile<2, 1, 32>(L, g, s); break;
-    case 3: launch_tile<1, 1, 32>(L, g, s); break;
-    case 4: launch_tile<1, 1, 16>(L, g, s); break;
-    default: return hipErrorInvalidValue;
+#define AVC_GEMM_VARIANT(I, PREC, WM, WN, WGM, WGN, KC, NAME) \
+    case I:                                                   \
+        launch_variant<PREC, WM, WN, WGM, WGN, KC>(L, g, s);  \
+        break;
+#include "avc_gemm_variants.h"
+#undef AVC_GEMM_VARIANT
+    default:
+        return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
@@ -850,7 +905,7 @@ static std::string tune_key(avc_ctx* ctx, const Plan& pl, size_t li) {
     char buf[256];
     const avc_se_cfg& c = ctx->cfg;
     snprintf(buf, sizeof(buf), "B%d_T%d_ch%d_%d_%d_nb%d_%s_l%zu", ctx->ws.B, ctx->ws.T, c.c_in, c.c_h, c.c_bank,
-             c.n_conv_blocks, &pl == &ctx->ws.fwd ? "fwd" : "iter", li);
+             c.n_conv_blocks, &pl == &ctx->ws.fwd ? "fwd" : (&pl == &ctx->ws.iter ? "iter" : "iterbf16"), li);
     return buf;
 }
 
@@ -875,7 +930,9 @@ static int autotune(avc_ctx* ctx, Plan& pl) {
     for (size_t li = 0; li < pl.launches.size(); ++li) {
         if (pl.launches[li].kind != L_GEMM) continue;
         auto it = cache.find(tune_key(ctx, pl, li));
-        if (it == cache.end() || it->second < 0 || it->second >= NVARIANTS) all_cached = false;
+        if (it == cache.end() || it->second < 0 || it->second >= NVARIANTS ||
+            VARIANTS[it->second].prec != pl.launches[li].prec)
+            all_cached = false;
     }
     if (all_cached) {
         for (size_t li = 0; li < pl.launches.size(); ++li)
@@ -890,6 +947,7 @@ static int autotune(avc_ctx* ctx, Plan& pl) {
         int best = L.variant;
         float best_ms = 1e30f;
         for (int v = 0; v < NVARIANTS; ++v) {
+            if (VARIANTS[v].prec != L.prec) continue;
             float t[3];
             HIPCHK(launch_gemm(L, v, ctx->stream));
             for (int r = 0; r < 3; ++r) {
@@ -940,6 +998,13 @@ static int run_plan(avc_ctx* ctx, const Plan& pl, bool prof) {
             s.first += ms;
             s.second += L.flop;
             ctx->prof_n[nm] += 1;
+            if (getenv("AVC_PROFILE_ROLES")) {   // per-layer breakdown (diagnostics)
+                const std::string rn = "role:" + L.name + "|" + nm;
+                auto& r = ctx->prof[rn];
+                r.first += ms;
+                r.second += L.flop;
+                ctx->prof_n[rn] += 1;
+            }
             hipEventDestroy(a);
             hipEventDestroy(b);
         }
@@ -992,13 +1057,24 @@ extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* ad
     avc_attack_opts o{};
     o.use_graph = 1;
     if (opts) o = *opts;
-    if (o.precision != AVC_PREC_FP32) return fail("precision %d not available in this build", o.precision);
+    if (o.precision != AVC_PREC_FP32 && o.precision != AVC_PREC_BF16) return fail("bad precision %d", o.precision);
     if (o.reduction != AVC_REDUCE_INDEPENDENT && o.reduction != AVC_REDUCE_MEAN)
         return fail("bad reduction %d", o.reduction);
     hipStream_t us = (hipStream_t)stream;
     if (ensure_ws(ctx, B, T, n_iters)) return 1;
-    if (begin_call(ctx, us)) return 1;
     Workspace& ws = ctx->ws;
+    const bool bf16 = o.precision == AVC_PREC_BF16;
+    if (bf16 && ws.iter_bf16.launches.empty()) {
+        if (plan_forward(ctx, ws, ws.iter_bf16, ws.adv.p, true, PREC_BF16)) return 1;
+        if (plan_backward(ctx, ws, ws.iter_bf16, PREC_BF16)) return 1;
+        const float scal0[4] = {0.1f, 0.f, 0.f, 0.f};
+        HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
+        HIPCHK(hipMemset(ws.step, 0, sizeof(int)));
+        if (autotune(ctx, ws.iter_bf16)) return 1;
+    }
+    Plan& iter = bf16 ? ws.iter_bf16 : ws.iter;
+    hipGraphExec_t& graph = bf16 ? ws.graph_bf16 : ws.graph;
+    if (begin_call(ctx, us)) return 1;
     const avc_se_cfg& c = ctx->cfg;
     const size_t X = (size_t)B * c.c_in * T;
     const float gscale = (float)(2.0 / (o.reduction == AVC_REDUCE_MEAN ? (double)B * c.c_out : (double)c.c_out));
@@ -1038,7 +1114,7 @@ extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* ad
         HIPCHK(hipEventCreate(&b));
         HIPCHK(hipEventRecord(a, ctx->stream));
         for (int it = 0; it < n_iters; ++it)
-            if (run_plan(ctx, ws.iter, true)) return 1;
+            if (run_plan(ctx, iter, true)) return 1;
         HIPCHK(hipEventRecord(b, ctx->stream));
         HIPCHK(hipEventSynchronize(b));
         float ms = 0;
@@ -1047,25 +1123,25 @@ extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* ad
         ctx->prof_iters += n_iters;
         hipEventDestroy(a);
         hipEventDestroy(b);
-    } else if (o.use_graph && n_iters > 0) {
-        if (!ws.graph) {
+    } else if (o.use_graph && n_iters > 0 && !(getenv("AVC_NO_GRAPH") && getenv("AVC_NO_GRAPH")[0] == '1')) {
+        if (!graph) {
             hipGraph_t g;
             HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-            int rc = run_plan(ctx, ws.iter, false);
+            int rc = run_plan(ctx, iter, false);
             hipError_t e = hipStreamEndCapture(ctx->stream, &g);
             if (rc) return 1;
             if (e != hipSuccess) return fail("graph capture: %s", hipGetErrorString(e));
-            e = hipGraphInstantiate(&ws.graph, g, nullptr, nullptr, 0);
+            e = hipGraphInstantiate(&graph, g, nullptr, nullptr, 0);
             hipGraphDestroy(g);
             if (e != hipSuccess) {
-                ws.graph = nullptr;
+                graph = nullptr;
                 return fail("graph instantiate: %s", hipGetErrorString(e));
             }
         }
-        for (int it = 0; it < n_iters; ++it) HIPCHK(hipGraphLaunch(ws.graph, ctx->stream));
+        for (int it = 0; it < n_iters; ++it) HIPCHK(hipGraphLaunch(graph, ctx->stream));
     } else {
         for (int it = 0; it < n_iters; ++it)
-            if (run_plan(ctx, ws.iter, false)) return 1;
+            if (run_plan(ctx, iter, false)) return 1;
     }
     HIPCHK(hipMemcpyAsync(out_adv, ws.adv.p, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     if (o.losses && n_iters > 0)
@@ -1081,7 +1157,8 @@ extern "C" int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_f
     if (ctx->prof_iters == 0) return fail("no profiled iterations");
     if (ms_per_iter) *ms_per_iter = ctx->prof_iter_ms / ctx->prof_iters;
     double f = 0;
-    for (auto& kv : ctx->prof) f += kv.second.second;
+    for (auto& kv : ctx->prof)
+        if (kv.first.rfind("role:", 0) != 0) f += kv.second.second;
     if (gemm_flop_per_iter) *gemm_flop_per_iter = f / ctx->prof_iters;
     return 0;
 }

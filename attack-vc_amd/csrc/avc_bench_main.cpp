@@ -4,7 +4,7 @@
 // Weights/inputs are synthetic (uniform / normal from a fixed-seed generator):
 // kernel durations do not depend on the values.
 //
-//   avc_bench [B=256] [T=128] [n_iters=1500] [steps=1] [warmup=0]
+//   avc_bench [B=256] [T=128] [n_iters=1500] [steps=1] [warmup=0] [precision 0=fp32 1=bf16]
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -38,6 +38,7 @@ int main(int argc, char** argv) {
     const int n_iters = argc > 3 ? atoi(argv[3]) : 1500;
     const int steps = argc > 4 ? atoi(argv[4]) : 1;
     const int warmup = argc > 5 ? atoi(argv[5]) : 0;
+    const int prec = argc > 6 ? atoi(argv[6]) : AVC_PREC_FP32;
 
     avc_se_cfg cfg{};
     cfg.c_in = 80;
@@ -76,6 +77,7 @@ int main(int argc, char** argv) {
 
     avc_attack_opts o{};
     o.use_graph = 1;
+    o.precision = prec;
     for (int i = 0; i < warmup; ++i) CK(avc_emb_attack(ctx, vc, at, p0, B, T, 0.1f, n_iters, out, &o, nullptr));
     HK(hipDeviceSynchronize());
     auto t0 = std::chrono::steady_clock::now();
@@ -89,6 +91,21 @@ int main(int argc, char** argv) {
     printf("{\"B\": %d, \"T\": %d, \"n_iters\": %d, \"steps\": %d, \"s\": %.4f, \"utts_per_s\": %.3f, "
            "\"ms_per_iter\": %.4f, \"checksum\": %.6f}\n",
            B, T, n_iters, steps, s, B * steps / s, s * 1e3 / (steps * (double)n_iters), cs);
+    // per-kernel HIP-event profile of 3 iterations
+    CK(avc_set_profiling(ctx, 1));
+    CK(avc_emb_attack(ctx, vc, at, p0, B, T, 0.1f, 3, out, &o, nullptr));
+    HK(hipDeviceSynchronize());
+    double ms_it = 0, fl_it = 0;
+    CK(avc_get_profile(ctx, &ms_it, &fl_it));
+    printf("{\"profiled_ms_per_iter\": %.4f, \"flop_per_iter\": %.4e}\n", ms_it, fl_it);
+    for (int i = 0; i < avc_profile_kernel_count(ctx); ++i) {
+        char name[128];
+        long n = 0;
+        double tms = 0, tfl = 0;
+        CK(avc_profile_kernel(ctx, i, name, sizeof(name), &n, &tms, &tfl));
+        printf("{\"kernel\": \"%s\", \"launches_per_iter\": %.1f, \"avg_ms\": %.4f, \"tflops\": %.2f}\n", name,
+               n / 3.0, tms / n, tfl / (tms * 1e-3) / 1e12);
+    }
     avc_destroy(ctx);
     return 0;
 }

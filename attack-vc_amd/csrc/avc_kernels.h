@@ -7,12 +7,14 @@
 
 namespace avc {
 
-constexpr int KSEG = 32;        // K-segment granule: a segment's rows are padded to it, so no K chunk
-                                // (16 or 32 rows) ever straddles two segments
-constexpr int KALIGN = 32;      // A matrices carry zero rows up to a multiple of the largest K chunk
+constexpr int KSEG = 64;        // K-segment granule: a segment's rows are padded to it, so no K chunk
+                                // (32 or 64 rows) ever straddles two segments
+constexpr int KALIGN = 64;      // A matrices carry zero rows up to a multiple of the largest K chunk
 constexpr int MAX_SEGS = 8;
 
 // How the im2col B-operand rows of one K segment are gathered from HBM.
+enum Prec : int32_t { PREC_F32 = 0, PREC_BF16 = 1 };
+
 enum SegMode : int32_t {
     SEG_FWD = 0,   // x_pad[c][t*stride + j] with reflect padding (models.py:10-30)
     SEG_BWD = 1,   // adjoint: zero-dilated dY, flipped taps, reflect-pad fold (dY already
@@ -57,8 +59,11 @@ struct Problem {
     int32_t M, Mpad, N, K;     // GEMM: C[M][N] = A[M][K] * B[K][N]; K = end of the last segment
     int32_t T_out;             // columns per utterance (N = B*T_out)
     int32_t nseg;
+    int32_t Kld;               // row stride of A (K rounded up to KALIGN; zero columns)
+    int32_t pad0_;
     int32_t epi, act;
-    const float* At;           // [K][Mpad]
+    const float* At;           // A row-major [Mpad][Kld] (k contiguous), fp32
+    const void* Ab;            // the same A in bf16 (round-to-nearest-even)
     const float* bias;         // [M] or null
     float* out0; int32_t out0_C, out0_coff;
     float* out1; int32_t out1_C, split;

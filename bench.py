@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--n-iters", type=int, default=1500)
     ap.add_argument("--eps", type=float, default=0.1)
-    ap.add_argument("--precision", default="fp32", choices=["fp32"])
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")

@@ -91,11 +91,16 @@ int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, cons
                    int B, int T, float eps, int n_iters, float* out_adv,
                    const avc_attack_opts* opts, void* stream);
 
-/* Average device duration (ms) of the dominant kernel class over the last
- * avc_emb_attack call on this ctx, measured with HIP events on the ctx's
- * stream when profiling is enabled via avc_set_profiling(ctx, 1). */
+/* Per-launch HIP-event profiling (bench.py's roofline).  While enabled, the
+ * attack loop runs without graph replay and brackets every kernel launch with
+ * HIP events on the ctx's stream, accumulating per-kernel-name launch counts,
+ * device milliseconds and algorithmic FLOPs (weight gradients excluded). */
 int avc_set_profiling(avc_ctx* ctx, int enable);
+/* average ms per profiled attack iteration and algorithmic FLOP per iteration */
 int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_flop_per_iter);
+int avc_profile_kernel_count(avc_ctx* ctx);
+int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len, long* launches, double* total_ms,
+                       double* total_flop);
 
 const char* avc_last_error(void);
 const char* avc_version(void);

@@ -23,6 +23,12 @@ timeout -k 10 600 python bench.py --steps ${STEPS:-2} --warmup 1 --cpu-seconds 1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
 [ $rc -eq 0 ] || stop bench $rc
 
+if [ "${BF16:-1}" = "1" ]; then
+timeout -k 10 600 python bench.py --steps ${STEPS:-2} --warmup 1 --precision bf16 --no-cpu-baseline > gpurun_out/bench_bf16.log 2>&1
+rc=$?; echo "bench bf16 rc=$rc"; tail -1 gpurun_out/bench_bf16.log
+[ $rc -eq 0 ] || stop bench_bf16 $rc
+fi
+
 if [ "${PROF:-1}" = "1" ]; then
   export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_native -o run --output-format csv -- \

@@ -160,3 +160,32 @@ def test_full_size_properties(gpu, golden):
                             p0[idx].cpu().numpy())
     d = np.abs(a[idx].detach().cpu().numpy() - ref)
     assert d.max() <= 1e-3 and d.mean() <= 1e-6
+
+
+def test_bf16_mode_tracks_fp32(gpu, golden):
+    """bf16 MFMA operands (fp32 accumulate, fp32 Adam state): SURVEY.md 8(c)
+    tolerances - one-step gradient cosine >= 0.99 vs the reference, adv within
+    2e-2 at n=100, final embedding loss within 5% of the fp32 reference's."""
+    z = golden("full_T128")
+    m = model_from_fixture(z).to(gpu)
+    adv, info = attack_utils.emb_attack(m, _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 100,
+                                        ptb0=_dev(z["emb_ptb0"]), precision="bf16", return_info=True)
+    g = info["grad0"].cpu().numpy().reshape(2, -1).astype(np.float64)
+    r = z["emb_grad0"].reshape(2, -1).astype(np.float64)
+    cos = (g * r).sum(1) / np.linalg.norm(g, axis=1) / np.linalg.norm(r, axis=1)
+    assert cos.min() >= 0.99, cos
+    assert np.abs(adv.detach().cpu().numpy() - z["emb_adv_n100"]).max() <= 2e-2
+    L = info["losses"].cpu().numpy().T[:, -1]
+    Lref = z["emb_losses_n1500"][:, 99]      # iteration 99 of the same trajectory
+    assert np.all(np.abs(L - Lref) <= 0.05 * np.abs(Lref)), (L, Lref)
+
+
+def test_bf16_batch_shard_invariance(gpu, golden):
+    z = golden("full_T128")
+    m = model_from_fixture(z).to(gpu)
+    g = torch.Generator().manual_seed(9)
+    vc, at, p0 = (torch.randn(32, 80, 128, generator=g).to(gpu) for _ in range(3))
+    full = attack_utils.emb_attack(m, vc, at, 0.1, 10, ptb0=p0, precision="bf16").detach()
+    lo = attack_utils.emb_attack(m, vc[:16], at[:16], 0.1, 10, ptb0=p0[:16], precision="bf16").detach()
+    hi = attack_utils.emb_attack(m, vc[16:], at[16:], 0.1, 10, ptb0=p0[16:], precision="bf16").detach()
+    assert torch.equal(torch.cat([lo, hi]), full)
