@@ -17,7 +17,8 @@
 
 namespace avc {
 template <int PREC, int WM, int WN, int WGM, int WGN, int KC, int MODE, int STRIDE>
-__global__ void conv_gemm(const Problem* __restrict__ probs);
+__global__ void conv_gemm(const Problem* __restrict__ probs, int ksplit);
+__global__ void splitk_reduce(const Problem* __restrict__ probs, int ksplit);
 __global__ void se_head(HeadArgs A);
 __global__ void attack_init(const float* vc, const float* ptb0, float* ptb, float* m, float* v, float* adv,
                             float eps, size_t n);
@@ -46,6 +47,7 @@ static int fail(const char* fmt, ...) {
 
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 static inline int cdiv(int x, int m) { return (x + m - 1) / m; }
+constexpr int KSPLIT_MAX = 4;
 
 namespace {
 
@@ -83,8 +85,10 @@ struct Launch {
     int kind;
     int variant = 0;             // L_GEMM: index into VARIANTS
     int prec = PREC_F32;         // L_GEMM: operand precision of the MFMAs
+    int ksplit = 1;              // L_GEMM: split-K factor (then + a splitk_reduce launch)
     int mode = 0, stride = 1;    // L_GEMM: loader specialisation shared by all its problems
     int maxM = 0, maxN = 0;      // L_GEMM: grid extents over its problems
+    int minMpad = 0;             // L_GEMM: smallest A row count (a tile may not read past it)
     dim3 grid, block;
     size_t shmem = 0;
     Problem* dprobs = nullptr;   // device problem table (L_GEMM*)
@@ -104,7 +108,7 @@ struct Workspace {
     std::vector<int> Tl;        // T_0..T_n (per conv block input lengths)
     DevBuf xin, adv, vc, ptb, m, v, bank, h0, gbank, gxd, g1, ghx, ghy, gmx, gmy, emb_fwd, org, tgt, grad0;
     std::vector<DevBuf> a1, a2, hb;   // per block
-    DevBuf losses, table, scal;
+    DevBuf losses, table, scal, slab;
     int iters_cap = 0;
     int* step = nullptr;
     Plan fwd, iter, iter_bf16;
@@ -444,7 +448,7 @@ static void free_plans(Workspace& ws) {
 static void free_ws(Workspace& ws) {
     free_plans(ws);
     DevBuf* bufs[] = {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.bank, &ws.h0, &ws.gbank, &ws.gxd,
-                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal};
+                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal, &ws.slab};
     for (DevBuf* b : bufs) dfree(*b);
     for (auto& b : ws.a1) dfree(b);
     for (auto& b : ws.a2) dfree(b);
@@ -520,16 +524,38 @@ static void add_seg(Problem& p, const Seg& s) {
 
 static dim3 gemm_grid(const Launch& L, int variant) {
     const Variant& v = VARIANTS[variant];
-    return dim3(cdiv(L.maxN, v.nt()), cdiv(L.maxM, v.mt()), L.nprob);
+    return dim3(cdiv(L.maxN, v.nt()), cdiv(L.maxM, v.mt()), L.nprob * L.ksplit);
+}
+
+// Split-K factor of a layer.  It may depend on the layer's shape per utterance
+// (T_out, K, M) but NOT on the batch size, so that a batch and any shard of it
+// sum every output in the same order (bitwise shard invariance); the split
+// boundaries are multiples of KALIGN rows, so the tile variant cannot move them.
+static int choose_ksplit(const Problem& p, int nprob) {
+    if (const char* e = getenv("AVC_KSPLIT")) return std::max(1, std::min(KSPLIT_MAX, atoi(e)));
+    if (nprob > 1 || p.M > 128) return 1;
+    const int kb = p.K / KALIGN;                 // K in KALIGN blocks
+    int ks = 1;
+    if (p.K >= 2048) ks = 4;                     // conv-bank dgrad (K = 4608 at the AdaIN-VC config)
+    else if (p.T_out <= 32) ks = 4;
+    else if (p.T_out <= 64) ks = 2;
+    return std::max(1, std::min(ks, kb));
+}
+
+// A variant may run a launch only if its M tiles stay inside every A matrix
+// (rows up to Mpad are allocated; the kernel reads whole M tiles of A).
+static bool variant_fits(const Launch& L, int v) {
+    const int mt = VARIANTS[v].mt();
+    return VARIANTS[v].prec == L.prec && cdiv(L.maxM, mt) * mt <= L.minMpad;
 }
 
 // default tile before autotuning: the largest tile of this precision whose grid
 // still has >= 512 workgroups (2 per CU), else the smallest tile
-static int default_variant(const std::vector<Problem>& ps, int prec) {
+static int default_variant(const Launch& L, const std::vector<Problem>& ps, int prec) {
     int best = -1, small = -1;
     long best_area = 0, small_area = 1L << 40;
     for (int v = 0; v < NVARIANTS; ++v) {
-        if (VARIANTS[v].prec != prec) continue;
+        if (VARIANTS[v].prec != prec || !variant_fits(L, v)) continue;
         const long area = (long)VARIANTS[v].mt() * VARIANTS[v].nt();
         long wgs = 0;
         for (auto& p : ps) wgs += (long)cdiv(p.M, VARIANTS[v].mt()) * cdiv(p.N, VARIANTS[v].nt());
@@ -547,7 +573,20 @@ static int default_variant(const std::vector<Problem>& ps, int prec) {
 
 static int add_gemm(avc_ctx* ctx, Plan& pl, std::vector<Problem> ps, double flop, const std::string& what,
                     int prec) {
-    int gx = 0, gy = 0;
+    int gx = 0, gy = 0, minMpad = 0;
+    const int ksplit_req = choose_ksplit(ps[0], (int)ps.size());
+    int ksplit = 1;
+    if (ksplit_req > 1) {
+        Problem& p = ps[0];
+        p.ksplit_rows = rup(cdiv(p.K, ksplit_req), KALIGN);
+        ksplit = cdiv(p.K, p.ksplit_rows);
+        if (ksplit > 1) {
+            if ((size_t)ksplit * p.M * p.N > ctx->ws.slab.n) return fail("internal: split-K slab too small");
+            p.slab = ctx->ws.slab.p;
+        } else {
+            p.ksplit_rows = 0;
+        }
+    }
     for (auto& p : ps) {
         auto it = ctx->bf16_of.find(p.At);
         if (it == ctx->bf16_of.end()) return fail("internal: no bf16 copy of an A matrix");
@@ -560,6 +599,7 @@ static int add_gemm(avc_ctx* ctx, Plan& pl, std::vector<Problem> ps, double flop
         if (p.Kld != rup(p.K, KALIGN)) return fail("internal: Kld %d for K %d", p.Kld, p.K);
         gx = std::max(gx, p.N);
         gy = std::max(gy, p.M);
+        minMpad = minMpad ? std::min(minMpad, p.Mpad) : p.Mpad;
     }
     Problem* d = nullptr;
     HIPCHK(hipMalloc(&d, ps.size() * sizeof(Problem)));
@@ -568,11 +608,14 @@ static int add_gemm(avc_ctx* ctx, Plan& pl, std::vector<Problem> ps, double flop
     Launch L;
     L.kind = L_GEMM;
     L.prec = prec;
-    L.variant = default_variant(ps, prec);
-    L.mode = ps[0].seg[0].mode;
-    L.stride = ps[0].seg[0].stride;
+    L.ksplit = ksplit;
     L.maxN = gx;
     L.maxM = gy;
+    L.minMpad = minMpad;
+    L.variant = default_variant(L, ps, prec);
+    if (L.variant < 0) return fail("internal: no GEMM variant fits %s", what.c_str());
+    L.mode = ps[0].seg[0].mode;
+    L.stride = ps[0].seg[0].stride;
     L.block = dim3(256);
     L.dprobs = d;
     L.nprob = (int)ps.size();
@@ -829,6 +872,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         }
         HIPCHK(hipMalloc(&ws.step, sizeof(int)));
         rc |= dalloc(ws.scal, 4);
+        rc |= dalloc(ws.slab, (size_t)KSPLIT_MAX * std::max(c.c_h, c.c_in) * B * T);
         if (rc) return 1;
     }
     const int cap = std::max(n_iters, std::max(ws.iters_cap, 1));
@@ -853,7 +897,8 @@ template <int PREC, int WM, int WN, int WGM, int WGN, int KC>
 static void launch_variant(const Launch& L, dim3 g, hipStream_t s) {
     const dim3 blk(64 * WGM * WGN);
     const int st = (L.stride == 1 || L.stride == 2) ? L.stride : 0;
-#define AVC_L(MODE, ST) hipLaunchKernelGGL((conv_gemm<PREC, WM, WN, WGM, WGN, KC, MODE, ST>), g, blk, 0, s, L.dprobs)
+#define AVC_L(MODE, ST) \
+    hipLaunchKernelGGL((conv_gemm<PREC, WM, WN, WGM, WGN, KC, MODE, ST>), g, blk, 0, s, L.dprobs, L.ksplit)
     if (L.mode == SEG_FWD) {
         if (st == 1) AVC_L(SEG_FWD, 1);
         else if (st == 2) AVC_L(SEG_FWD, 2);
@@ -867,6 +912,7 @@ static void launch_variant(const Launch& L, dim3 g, hipStream_t s) {
 }
 
 static hipError_t launch_gemm(const Launch& L, int variant, hipStream_t s) {
+    if (variant < 0 || variant >= NVARIANTS || !variant_fits(L, variant)) return hipErrorInvalidValue;
     const dim3 g = gemm_grid(L, variant);
     switch (variant) {
 #define AVC_GEMM_VARIANT(I, PREC, WM, WN, WGM, WGN, KC, NAME) \
@@ -877,6 +923,11 @@ static hipError_t launch_gemm(const Launch& L, int variant, hipStream_t s) {
 #undef AVC_GEMM_VARIANT
     default:
         return hipErrorInvalidValue;
+    }
+    if (L.ksplit > 1) {
+        const long groups = (long)L.maxM * cdiv(L.maxN, 4);
+        hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)cdiv((int)groups, 256), 1, L.nprob), dim3(256), 0, s,
+                           L.dprobs, L.ksplit);
     }
     return hipGetLastError();
 }
@@ -931,7 +982,7 @@ static int autotune(avc_ctx* ctx, Plan& pl) {
         if (pl.launches[li].kind != L_GEMM) continue;
         auto it = cache.find(tune_key(ctx, pl, li));
         if (it == cache.end() || it->second < 0 || it->second >= NVARIANTS ||
-            VARIANTS[it->second].prec != pl.launches[li].prec)
+            !variant_fits(pl.launches[li], it->second))
             all_cached = false;
     }
     if (all_cached) {
@@ -947,7 +998,7 @@ static int autotune(avc_ctx* ctx, Plan& pl) {
         int best = L.variant;
         float best_ms = 1e30f;
         for (int v = 0; v < NVARIANTS; ++v) {
-            if (VARIANTS[v].prec != L.prec) continue;
+            if (!variant_fits(L, v)) continue;
             float t[3];
             HIPCHK(launch_gemm(L, v, ctx->stream));
             for (int r = 0; r < 3; ++r) {

@@ -265,7 +265,7 @@ __device__ __forceinline__ bool epilogue4(const Problem& P, int m, int b, int t,
 
 // WM x WN 32x32 fragments per wave, WGM x WGN waves per workgroup, K chunk KC.
 template <int PREC, int WM, int WN, int WGM, int WGN, int KC, int MODE, int STRIDE>
-__global__ void __launch_bounds__(64 * WGM * WGN) conv_gemm(const Problem* __restrict__ probs) {
+__global__ void __launch_bounds__(64 * WGM * WGN) conv_gemm(const Problem* __restrict__ probs, int ksplit) {
     using E = typename PrecT<PREC>::T;
     constexpr int NTHR = 64 * WGM * WGN;
     constexpr int MT = 32 * WM * WGM, NT = 32 * WN * WGN;
@@ -283,9 +283,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_gemm(const Problem* __res
     static_assert((MT * KC / AVEC) % NTHR == 0, "A loader shape");
     static_assert(PREC == PREC_F32 ? KC % 8 == 0 : KC % 16 == 0, "K chunk vs MFMA K");
 
-    const Problem& P = probs[blockIdx.z];
+    // blockIdx.z = problem * ksplit + split (split-K: this WG sums K rows
+    // [split*ksplit_rows, (split+1)*ksplit_rows) into a slab; splitk_reduce finishes)
+    const int split = blockIdx.z % ksplit;
+    const Problem& P = probs[blockIdx.z / ksplit];
     const int m0 = blockIdx.y * MT, n0 = blockIdx.x * NT;
-    if (P.tick && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(P.tick, 1);
+    if (P.tick && split == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(P.tick, 1);
     if (m0 >= P.M || n0 >= P.N) return;
 
     __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
@@ -295,7 +298,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_gemm(const Problem* __res
     const int wm = wave / WGN, wn = wave % WGN;
     const int r32 = lane & 31, h = lane >> 5;
 
-    const int N = P.N, T_out = P.T_out, Kend = P.K, Kld = P.Kld, nseg = P.nseg, act = P.act;
+    const int N = P.N, T_out = P.T_out, Kend = P.K, Kld = P.Kld, nseg = P.nseg, act = P.act, Mpad = P.Mpad;
     const E* __restrict__ Ag = reinterpret_cast<const E*>(PREC == PREC_F32 ? (const void*)P.At : P.Ab);
 
     // B loader: lanes <-> columns n; each thread owns BPASS consecutive K rows of the
@@ -330,7 +333,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_gemm(const Problem* __res
             if (AVC_ABLATE & 4) {
                 areg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
             } else {
-                const E* src = Ag + (size_t)(m0 + r) * Kld + k0 + c * AVEC;
+                // rows past Mpad are never allocated: clamp (their outputs are discarded)
+                const E* src = Ag + (size_t)min(m0 + r, Mpad - 1) * Kld + k0 + c * AVEC;
                 areg[i] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
                     (const __attribute__((address_space(1))) E*)src);
             }
@@ -466,16 +470,23 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_gemm(const Problem* __res
 
     // software pipeline: LDS double buffer, gathers one chunk ahead in registers,
     // one barrier per chunk
-    const int nchunks = (Kend + KC - 1) / KC;
-    load_chunk(0);
-    store_chunk(0);
-    if (nchunks > 1) load_chunk(1);
-    __syncthreads();
-    for (int kc = 0; kc < nchunks; ++kc) {
-        if (!(AVC_ABLATE & 16)) compute(kc & 1);
-        if (kc + 1 < nchunks) store_chunk((kc + 1) & 1);
-        if (kc + 2 < nchunks) load_chunk(kc + 2);
+    int c_begin = 0, c_end = (Kend + KC - 1) / KC;
+    if (ksplit > 1) {
+        c_begin = split * (P.ksplit_rows / KC);
+        c_end = min(c_end, c_begin + P.ksplit_rows / KC);
+    }
+    if (c_begin < c_end) {
+        load_chunk(c_begin);
+        store_chunk(0);
+        if (c_begin + 1 < c_end) load_chunk(c_begin + 1);
         __syncthreads();
+        for (int kc = c_begin; kc < c_end; ++kc) {
+            const int st = (kc - c_begin) & 1;
+            if (!(AVC_ABLATE & 16)) compute(st);
+            if (kc + 1 < c_end) store_chunk(st ^ 1);
+            if (kc + 2 < c_end) load_chunk(kc + 2);
+            __syncthreads();
+        }
     }
 
     // Epilogue: each wave stages its accumulators as [32*WM rows][32*WN (+4) cols]
@@ -493,6 +504,23 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_gemm(const Problem* __res
     if (AVC_ABLATE & 2) return;
     constexpr int C4 = 8 * WN;                            // float4 groups per staged row
     const int mw = m0 + wm * 32 * WM, nw = n0 + wn * 32 * WN;
+    if (ksplit > 1) {   // raw partial sums; the epilogue runs in splitk_reduce
+        float* slab = P.slab + (size_t)split * P.M * N;
+        const bool v4 = (N & 3) == 0;
+#pragma unroll 1
+        for (int idx = lane; idx < 32 * WM * C4; idx += 64) {
+            const int row = idx / C4, c4 = idx - row * C4;
+            const int m = mw + row, nc = nw + 4 * c4;
+            if (m >= P.M || nc >= N) continue;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(&stg[row * EW + 4 * c4]);
+            if (v4) {
+                gstore<f32x4>(slab + (size_t)m * N + nc, v);
+            } else {
+                for (int e = 0; e < 4 && nc + e < N; ++e) slab[(size_t)m * N + nc + e] = v[e];
+            }
+        }
+        return;
+    }
     const bool vec_ok = (T_out & 3) == 0;
 #pragma unroll 1
     for (int idx = lane; idx < 32 * WM * C4; idx += 64) {
@@ -513,13 +541,44 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_gemm(const Problem* __res
     }
 }
 
-#define AVC_GEMM_MS(PREC, WM, WN, WGM, WGN, KC)                                                   \
-    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_FWD, 1>(const Problem*); \
-    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_FWD, 2>(const Problem*); \
-    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_FWD, 0>(const Problem*); \
-    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_BWD, 1>(const Problem*); \
-    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_BWD, 2>(const Problem*); \
-    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_BWD, 0>(const Problem*);
+// Split-K finish: sum the slabs in split order (deterministic; the split
+// boundaries are multiples of KALIGN rows, independent of the tile variant)
+// and apply the problem's fused epilogue, 4 consecutive columns per thread.
+__global__ void __launch_bounds__(256) splitk_reduce(const Problem* __restrict__ probs, int ksplit) {
+    const Problem& P = probs[blockIdx.z];
+    const int N = P.N, M = P.M, T = P.T_out;
+    const int ng = (N + 3) / 4;
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)M * ng) return;
+    const int m = (int)(gid / ng), nc = (int)(gid - (long)m * ng) * 4;
+    const size_t plane = (size_t)M * N;
+    const float* base = P.slab + (size_t)m * N + nc;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    const bool v4 = (N & 3) == 0;
+    for (int s = 0; s < ksplit; ++s) {
+        if (v4) {
+            v += gload<f32x4>(base + s * plane);
+        } else {
+            for (int e = 0; e < 4 && nc + e < N; ++e) v[e] += base[s * plane + e];
+        }
+    }
+    const int b = nc / T, t = nc - b * T;
+    if ((T & 3) == 0 && nc + 3 < N && epilogue4(P, m, b, t, v)) return;
+    for (int e = 0; e < 4; ++e) {
+        const int ne = nc + e;
+        if (ne >= N) break;
+        const int be = ne / T;
+        epilogue1(P, m, be, ne - be * T, v[e]);
+    }
+}
+
+#define AVC_GEMM_MS(PREC, WM, WN, WGM, WGN, KC)                                                        \
+    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_FWD, 1>(const Problem*, int); \
+    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_FWD, 2>(const Problem*, int); \
+    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_FWD, 0>(const Problem*, int); \
+    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_BWD, 1>(const Problem*, int); \
+    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_BWD, 2>(const Problem*, int); \
+    template __global__ void conv_gemm<PREC, WM, WN, WGM, WGN, KC, SEG_BWD, 0>(const Problem*, int);
 #define AVC_GEMM_VARIANT(I, PREC, WM, WN, WGM, WGN, KC, NAME) AVC_GEMM_MS(PREC, WM, WN, WGM, WGN, KC)
 #include "avc_gemm_variants.h"
 #undef AVC_GEMM_VARIANT

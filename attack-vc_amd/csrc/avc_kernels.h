@@ -60,7 +60,7 @@ struct Problem {
     int32_t T_out;             // columns per utterance (N = B*T_out)
     int32_t nseg;
     int32_t Kld;               // row stride of A (K rounded up to KALIGN; zero columns)
-    int32_t pad0_;
+    int32_t ksplit_rows;       // split-K: rows per split (multiple of KALIGN); 0 = no split
     int32_t epi, act;
     const float* At;           // A row-major [Mpad][Kld] (k contiguous), fp32
     const void* Ab;            // the same A in bf16 (round-to-nearest-even)
@@ -76,6 +76,7 @@ struct Problem {
     const float* scal;         // per-call scalars: [0] = attack eps, [1] = loss-grad scale
     int32_t table_len;         // Adam table entries (step is clamped into [1, table_len])
     int32_t pad2_;
+    float* slab;               // split-K partial sums [ksplit][M][N] (fp32), reduced in order
     AdamArgs adam;
     Seg seg[MAX_SEGS];
 };

@@ -17,18 +17,25 @@ namespace avc {
 // ---------------------------------------------------------------------------------
 constexpr int HU = 16;   // utterances per workgroup (the N of the 16x16x4 MFMA)
 
-// Y[row][u] = act(sum_k W[row][k] X[k][u] + bias[row]) for rows of wave `wave`.
-// Wpk: fragment-packed A, [M/16][K/4][64] with A[16*mt + (l&15)][4*kk + (l>>4)].
-// mode: 0 = ReLU/LReLU (act), 2 = identity.
-__device__ __forceinline__ void head_gemm(const float* __restrict__ Wpk, int M, int K,
-                                          const float* X, float* Y, const float* __restrict__ bias,
-                                          int act, bool apply_act, int wave, int lane) {
+// A wave's A fragments for one head layer: rows [16*wave, 16*wave+16) of the
+// fragment-packed weights [M/16][K/4][64] (A[16*mt + (l&15)][4*kk + (l>>4)]);
+// K <= 128 -> 32 values per lane, all loads issued at once.
+struct HeadW {
+    float a[32];
+};
+
+__device__ __forceinline__ void head_load(HeadW& w, const float* __restrict__ Wpk, int M, int K, int wave, int lane) {
     if (wave * 16 >= M) return;
     const float* Wt = Wpk + (size_t)wave * (K / 4) * 64;
-    // all of this wave's A fragments in flight at once (K <= 128 -> <= 32 per lane)
-    float a[32];
 #pragma unroll
-    for (int kk = 0; kk < 32; ++kk) a[kk] = (4 * kk < K) ? Wt[kk * 64 + lane] : 0.f;
+    for (int kk = 0; kk < 32; ++kk) w.a[kk] = (4 * kk < K) ? Wt[kk * 64 + lane] : 0.f;
+}
+
+// Y[row][u] = (act)(sum_k W[row][k] X[k][u] (+ bias[row])) for this wave's 16 rows.
+__device__ __forceinline__ void head_mma(const HeadW& w, int M, int K, const float* X, float* Y,
+                                         const float* __restrict__ bias, int act, bool apply_act, int wave,
+                                         int lane) {
+    if (wave * 16 >= M) return;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     const int hh = lane >> 4, col = lane & 15;
 #pragma unroll
@@ -36,8 +43,8 @@ __device__ __forceinline__ void head_gemm(const float* __restrict__ Wpk, int M, 
         if (4 * kk < K) {
             const float b0 = X[(4 * kk + hh) * HU + col];
             const float b1 = X[(4 * kk + 4 + hh) * HU + col];
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk + 1], b1, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a[kk], b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a[kk + 1], b1, acc1, 0, 0, 0);
         }
     }
 #pragma unroll
@@ -50,6 +57,16 @@ __device__ __forceinline__ void head_gemm(const float* __restrict__ Wpk, int M, 
     }
 }
 
+// The head as a chain of NL = 4*nd + 2 small GEMM steps; step i+1's weights are
+// loaded while step i computes (register double buffer, unrolled by two so both
+// buffers are statically indexed):
+//   fwd i <  2nd : Y_i = act(W_i X + b_i), X = e (i even) or Y_{i-1}; e += Y_i (i odd)
+//                  (dense_blocks, models.py:307-325)
+//   fwd i == 2nd : EMB = W_out e + b_out                       (models.py:342)
+//   [loss + d loss / d EMB -> GA]                              (attack_utils.py:81)
+//   bwd i == nf  : GB = W_out^T GA
+//   bwd j even   : GA = W_{2l+1}^T (GB * act'(Y_{2l+1})) * act'(Y_{2l})
+//   bwd j odd    : GB += W_{2l}^T GA
 __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
     extern __shared__ float smem[];
     const int C = A.C, D = A.D, nd = A.n_dense;
@@ -64,36 +81,155 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int u0 = blockIdx.x * HU;
+    const size_t CC = (size_t)C * C;
+    const int nf = 2 * nd + 1;                          // forward steps
+    const int NL = A.mode == 0 ? nf : 2 * nf;           // + backward steps
 
-    // AdaptiveAvgPool1d(1) (models.py:275,340)
+    auto step_w = [&](int i, const float*& W, int& M, int& K) {
+        if (i < 2 * nd) {
+            W = A.Wp + i * CC, M = C, K = C;
+        } else if (i == 2 * nd) {
+            W = A.Wp + 2 * nd * CC, M = D, K = C;
+        } else if (i == nf) {
+            W = A.WpT + 2 * nd * CC, M = C, K = D;
+        } else {
+            const int j = i - nf - 1;                   // 0 .. 2nd-1
+            const int l = nd - 1 - j / 2;
+            W = A.WpT + (j % 2 == 0 ? 2 * l + 1 : 2 * l) * CC, M = C, K = C;
+        }
+    };
+
+    HeadW w0, w1;
+    {
+        const float* W;
+        int M, K;
+        step_w(0, W, M, K);
+        head_load(w0, W, M, K, wave, lane);
+    }
+
+    // AdaptiveAvgPool1d(1) (models.py:275,340): a row's loads all in flight at once
     for (int idx = tid; idx < C * HU; idx += blockDim.x) {
         const int u = idx / C, c = idx - u * C;
         const int b = u0 + u;
         float s = 0.f;
         if (b < A.B) {
             const float* p = A.hN + ((size_t)b * C + c) * A.TN;
-            for (int t = 0; t < A.TN; ++t) s += p[t];
+            int t = 0;
+            if ((A.TN & 3) == 0) {
+                for (; t + 32 <= A.TN; t += 32) {
+                    f32x4 q[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) q[e] = gload<f32x4>(p + t + 4 * e);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) s += q[e][0] + q[e][1] + q[e][2] + q[e][3];
+                }
+                for (; t + 4 <= A.TN; t += 4) {
+                    const f32x4 q = gload<f32x4>(p + t);
+                    s += q[0] + q[1] + q[2] + q[3];
+                }
+            }
+            for (; t < A.TN; ++t) s += p[t];
             s = s / (float)A.TN;
         }
         E[c * HU + u] = s;
     }
     __syncthreads();
 
-    // dense_blocks (models.py:307-325)
-    const size_t CC = (size_t)C * C;
-    for (int l = 0; l < nd; ++l) {
-        float* Y1 = Ys + (2 * l) * S;
-        float* Y2 = Ys + (2 * l + 1) * S;
-        head_gemm(A.Wp + (2 * l) * CC, C, C, E, Y1, A.bias + (2 * l) * C, A.act, true, wave, lane);
-        __syncthreads();
-        head_gemm(A.Wp + (2 * l + 1) * CC, C, C, Y1, Y2, A.bias + (2 * l + 1) * C, A.act, true, wave, lane);
-        __syncthreads();
-        for (int idx = tid; idx < C * HU; idx += blockDim.x) E[idx] = Y2[idx] + E[idx];
-        __syncthreads();
+    const float gscale = A.scal[1];
+    const int step_no = A.mode == 0 ? 0 : *A.step;
+
+    auto run_step = [&](int i, const HeadW& w) {
+        const float* W;
+        int M, K;
+        step_w(i, W, M, K);
+        if (i < 2 * nd) {
+            const float* X = (i % 2 == 0) ? E : Ys + (i - 1) * S;
+            head_mma(w, M, K, X, Ys + i * S, A.bias + i * C, A.act, true, wave, lane);
+            __syncthreads();
+            if (i % 2 == 1) {
+                for (int idx = tid; idx < C * HU; idx += blockDim.x) E[idx] = Ys[i * S + idx] + E[idx];
+                __syncthreads();
+            }
+        } else if (i == 2 * nd) {
+            head_mma(w, M, K, E, EMB, A.bias + 2 * nd * C, A.act, false, wave, lane);
+            __syncthreads();
+            if (A.mode == 0) return;
+            // loss = MSE(emb, tgt) - 0.1*MSE(emb, org); d loss/d emb = 2/N (e-tgt) - 0.1*2/N (e-org)
+            for (int idx = tid; idx < D * HU; idx += blockDim.x) {
+                const int d = idx / HU, u = idx - d * HU;
+                const int b = u0 + u;
+                float g = 0.f, q1 = 0.f, q2 = 0.f;
+                if (b < A.B) {
+                    const float e = EMB[idx];
+                    const float d1 = e - A.tgt[(size_t)b * D + d];
+                    const float d2 = e - A.org[(size_t)b * D + d];
+                    g = gscale * d1 + gscale * d2 * -0.1f;
+                    q1 = d1 * d1;
+                    q2 = d2 * d2;
+                }
+                GA[idx] = g;
+                GC[idx] = q1;
+                GB[idx] = q2;
+            }
+            __syncthreads();
+            // per-utterance loss: one wave per 2 utterances, lanes over d, fixed-order butterfly
+            if (A.losses && step_no >= 1 && step_no <= A.loss_len) {
+                for (int u = 2 * wave; u < 2 * wave + 2 && u < HU; ++u) {
+                    float s1 = 0.f, s2 = 0.f;
+                    for (int d = lane; d < D; d += 64) {
+                        s1 += GC[d * HU + u];
+                        s2 += GB[d * HU + u];
+                    }
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) {
+                        s1 += __shfl_xor(s1, o);
+                        s2 += __shfl_xor(s2, o);
+                    }
+                    const int b = u0 + u;
+                    if (lane == 0 && b < A.B)
+                        A.losses[(size_t)(step_no - 1) * A.B + b] = s1 / (float)D - 0.1f * (s2 / (float)D);
+                }
+            }
+            __syncthreads();
+        } else if (i == nf) {
+            head_mma(w, M, K, GA, GB, nullptr, 0, false, wave, lane);   // g_e
+            __syncthreads();
+        } else {
+            const int j = i - nf - 1;
+            const int l = nd - 1 - j / 2;
+            const float* Y1 = Ys + (2 * l) * S;
+            const float* Y2 = Ys + (2 * l + 1) * S;
+            if (j % 2 == 0) {
+                for (int idx = tid; idx < C * HU; idx += blockDim.x) GC[idx] = GB[idx] * act_d(Y2[idx], A.act);
+                __syncthreads();
+                head_mma(w, M, K, GC, GA, nullptr, 0, false, wave, lane);
+                __syncthreads();
+                for (int idx = tid; idx < C * HU; idx += blockDim.x) GA[idx] = GA[idx] * act_d(Y1[idx], A.act);
+                __syncthreads();
+            } else {
+                head_mma(w, M, K, GA, GC, nullptr, 0, false, wave, lane);
+                __syncthreads();
+                for (int idx = tid; idx < C * HU; idx += blockDim.x) GB[idx] = GB[idx] + GC[idx];
+                __syncthreads();
+            }
+        }
+    };
+
+    for (int i = 0; i < NL; i += 2) {
+        const float* W;
+        int M, K;
+        if (i + 1 < NL) {
+            step_w(i + 1, W, M, K);
+            head_load(w1, W, M, K, wave, lane);
+        }
+        run_step(i, w0);
+        if (i + 1 >= NL) break;
+        if (i + 2 < NL) {
+            step_w(i + 2, W, M, K);
+            head_load(w0, W, M, K, wave, lane);
+        }
+        run_step(i + 1, w1);
     }
-    // output_layer (models.py:342)
-    head_gemm(A.Wp + 2 * nd * CC, D, C, E, EMB, A.bias + 2 * nd * C, A.act, false, wave, lane);
-    __syncthreads();
 
     if (A.mode == 0) {
         for (int idx = tid; idx < D * HU; idx += blockDim.x) {
@@ -103,55 +239,7 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
         }
         return;
     }
-
-    // loss = MSE(emb, tgt) - 0.1*MSE(emb, org) (attack_utils.py:81) and its gradient
-    const int step = *A.step;
-    if (tid < HU) {
-        const int b = u0 + tid;
-        if (b < A.B && A.losses && step >= 1 && step <= A.loss_len) {
-            float s1 = 0.f, s2 = 0.f;
-            for (int d = 0; d < D; ++d) {
-                const float e = EMB[d * HU + tid];
-                const float d1 = e - A.tgt[(size_t)b * D + d];
-                const float d2 = e - A.org[(size_t)b * D + d];
-                s1 += d1 * d1;
-                s2 += d2 * d2;
-            }
-            A.losses[(size_t)(step - 1) * A.B + b] = s1 / (float)D - 0.1f * (s2 / (float)D);
-        }
-    }
-    const float gscale = A.scal[1];
-    for (int idx = tid; idx < D * HU; idx += blockDim.x) {
-        const int d = idx / HU, u = idx - d * HU;
-        const int b = u0 + u;
-        float g = 0.f;
-        if (b < A.B) {
-            const float e = EMB[idx];
-            g = gscale * (e - A.tgt[(size_t)b * D + d]) + gscale * (e - A.org[(size_t)b * D + d]) * -0.1f;
-        }
-        GA[idx] = g;
-    }
-    __syncthreads();
-
-    // backward through output_layer and the dense blocks (input gradient only)
-    const size_t offT_out = 2 * nd * CC;
-    head_gemm(A.WpT + offT_out, C, D, GA, GB, nullptr, 0, false, wave, lane);   // g_e
-    __syncthreads();
-    for (int l = nd - 1; l >= 0; --l) {
-        const float* Y1 = Ys + (2 * l) * S;
-        const float* Y2 = Ys + (2 * l + 1) * S;
-        for (int idx = tid; idx < C * HU; idx += blockDim.x) GC[idx] = GB[idx] * act_d(Y2[idx], A.act);
-        __syncthreads();
-        head_gemm(A.WpT + (2 * l + 1) * CC, C, C, GC, GA, nullptr, 0, false, wave, lane);
-        __syncthreads();
-        for (int idx = tid; idx < C * HU; idx += blockDim.x) GA[idx] = GA[idx] * act_d(Y1[idx], A.act);
-        __syncthreads();
-        head_gemm(A.WpT + (2 * l) * CC, C, C, GA, GC, nullptr, 0, false, wave, lane);
-        __syncthreads();
-        for (int idx = tid; idx < C * HU; idx += blockDim.x) GB[idx] = GB[idx] + GC[idx];
-        __syncthreads();
-    }
-    // d/d hN of the mean over time
+    // d/d hN of the mean over time, and its copy gated by the ReLU that produced h_N
     const int TN = A.TN;
     for (int u = 0; u < HU && u0 + u < A.B; ++u) {
         const size_t off = (size_t)(u0 + u) * C * TN;

@@ -103,6 +103,7 @@ def main():
     import attack_utils
     import avc_native
     import models
+    import shard
 
     torch.manual_seed(0)
     model = models.AdaInVC(FULL_CFG)           # random-init weights of the AdaIN-VC architecture
@@ -113,7 +114,7 @@ def main():
     vc_all = torch.randn(total, 80, T, generator=g)
     at_all = torch.randn(total, 80, T, generator=g)
     p0_all = torch.randn(total, 80, T, generator=torch.Generator().manual_seed(123))
-    sl = slice(rank * B, (rank + 1) * B)
+    sl = shard.shard_slice(total, rank, world)
     vc, at, p0 = (t[sl].contiguous().to(dev) for t in (vc_all, at_all, p0_all))
     del vc_all, at_all, p0_all
 
@@ -133,11 +134,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
     assert torch.isfinite(out).all()
 
     roof = None

@@ -1,0 +1,86 @@
+"""CPU (gloo, world_size 2): the multi-process sharding path of bench.py --
+contiguous utterance shards, max-over-ranks timing, host-side gather -- with the
+CPU oracle standing in for the per-rank compute (no GPU here)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import shard
+
+
+def test_shard_slice_covers_exactly():
+    for total in (0, 1, 7, 256, 2048, 2049):
+        for world in (1, 2, 3, 8):
+            got = []
+            for r in range(world):
+                sl = shard_slice_list(total, r, world)
+                got.extend(sl)
+            assert got == list(range(total)), (total, world)
+            sizes = [len(shard_slice_list(total, r, world)) for r in range(world)]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def shard_slice_list(total, r, world):
+    sl = shard.shard_slice(total, r, world)
+    return list(range(sl.start, sl.stop))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import json
+    from conftest import GOLDEN
+    from oracle import adain_vc as oracle
+    z = np.load(os.path.join(GOLDEN, "small_T32.npz"))
+    cfg = json.loads(str(z["config"]))
+    w = oracle.Weights({k[2:]: z[k] for k in z.files if k.startswith("w/")})
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(total, 80, 32, generator=g).numpy()
+    sl = shard.shard_slice(total, rank, world)
+    emb = np.concatenate([oracle.se_forward(w, cfg["SpeakerEncoder"], x[b:b + 1])[0]
+                          for b in range(sl.start, sl.stop)]) if sl.stop > sl.start else np.zeros((0, 32), np.float32)
+    full = shard.gather_shards(torch.from_numpy(emb), total, dist)
+    t = shard.max_over_ranks(float(rank + 1), dist)
+    if rank == 0:
+        q.put((full.numpy(), t))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total", [5, 6])
+def test_gloo_two_ranks_gather_and_max(total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    full, t = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # reference: the same per-utterance oracle in one process
+    import json
+    from conftest import GOLDEN
+    from oracle import adain_vc as oracle
+    z = np.load(os.path.join(GOLDEN, "small_T32.npz"))
+    cfg = json.loads(str(z["config"]))
+    w = oracle.Weights({k[2:]: z[k] for k in z.files if k.startswith("w/")})
+    x = torch.randn(total, 80, 32, generator=torch.Generator().manual_seed(3)).numpy()
+    ref = np.concatenate([oracle.se_forward(w, cfg["SpeakerEncoder"], x[b:b + 1])[0] for b in range(total)])
+    assert np.array_equal(full, ref)
+    assert t == 2.0

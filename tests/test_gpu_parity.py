@@ -189,3 +189,16 @@ def test_bf16_batch_shard_invariance(gpu, golden):
     lo = attack_utils.emb_attack(m, vc[:16], at[:16], 0.1, 10, ptb0=p0[:16], precision="bf16").detach()
     hi = attack_utils.emb_attack(m, vc[16:], at[16:], 0.1, 10, ptb0=p0[16:], precision="bf16").detach()
     assert torch.equal(torch.cat([lo, hi]), full)
+
+
+def test_multi_gpu_driver_matches_single(gpu, golden):
+    """shard.emb_attack_multi_gpu (one host thread per device) == one call; run
+    here with the same device listed twice (the box has one GPU)."""
+    import shard
+    z = golden("small_T32")
+    m = model_from_fixture(z).to(gpu)
+    g = torch.Generator().manual_seed(4)
+    vc, at, p0 = (torch.randn(5, 80, 32, generator=g).to(gpu) for _ in range(3))
+    one = attack_utils.emb_attack(m, vc, at, 0.1, 8, ptb0=p0).detach()
+    two = shard.emb_attack_multi_gpu([m, m], vc, at, 0.1, 8, ptb0=p0).detach()
+    assert torch.equal(one, two)
