@@ -2,6 +2,7 @@
 // and launch plans, the on-device attack loop (hipGraph replay per iteration),
 // and per-kernel HIP-event profiling for bench.py's roofline.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -47,7 +48,6 @@ static int fail(const char* fmt, ...) {
 
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 static inline int cdiv(int x, int m) { return (x + m - 1) / m; }
-constexpr int KSPLIT_MAX = 4;
 
 namespace {
 
@@ -893,12 +893,30 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     return 0;
 }
 
+// Kernel-timestamp events for profiled launches: hipExtLaunchKernelGGL stamps the
+// dispatch packet itself (the same start/end rocprofv3 reports), so per-kernel
+// averages carry no event-record overhead.  Null => plain launch (graph capture).
+struct KEv {
+    hipEvent_t gemm0 = nullptr, gemm1 = nullptr;   // conv_gemm
+    hipEvent_t red0 = nullptr, red1 = nullptr;     // splitk_reduce (when ksplit > 1)
+};
+
+template <typename F, typename... Args>
+static void klaunch(const KEv* ev, bool reduce, F kernel, dim3 g, dim3 blk, unsigned shmem, hipStream_t s,
+                    Args... args) {
+    if (ev)
+        hipExtLaunchKernelGGL(kernel, g, blk, shmem, s, reduce ? ev->red0 : ev->gemm0,
+                              reduce ? ev->red1 : ev->gemm1, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, g, blk, shmem, s, args...);
+}
+
 template <int PREC, int WM, int WN, int WGM, int WGN, int KC>
-static void launch_variant(const Launch& L, dim3 g, hipStream_t s) {
+static void launch_variant(const Launch& L, dim3 g, hipStream_t s, const KEv* ev) {
     const dim3 blk(64 * WGM * WGN);
     const int st = (L.stride == 1 || L.stride == 2) ? L.stride : 0;
 #define AVC_L(MODE, ST) \
-    hipLaunchKernelGGL((conv_gemm<PREC, WM, WN, WGM, WGN, KC, MODE, ST>), g, blk, 0, s, L.dprobs, L.ksplit)
+    klaunch(ev, false, conv_gemm<PREC, WM, WN, WGM, WGN, KC, MODE, ST>, g, blk, 0, s, L.dprobs, L.ksplit)
     if (L.mode == SEG_FWD) {
         if (st == 1) AVC_L(SEG_FWD, 1);
         else if (st == 2) AVC_L(SEG_FWD, 2);
@@ -911,13 +929,13 @@ static void launch_variant(const Launch& L, dim3 g, hipStream_t s) {
 #undef AVC_L
 }
 
-static hipError_t launch_gemm(const Launch& L, int variant, hipStream_t s) {
+static hipError_t launch_gemm(const Launch& L, int variant, hipStream_t s, const KEv* ev = nullptr) {
     if (variant < 0 || variant >= NVARIANTS || !variant_fits(L, variant)) return hipErrorInvalidValue;
     const dim3 g = gemm_grid(L, variant);
     switch (variant) {
 #define AVC_GEMM_VARIANT(I, PREC, WM, WN, WGM, WGN, KC, NAME) \
     case I:                                                   \
-        launch_variant<PREC, WM, WN, WGM, WGN, KC>(L, g, s);  \
+        launch_variant<PREC, WM, WN, WGM, WGN, KC>(L, g, s, ev); \
         break;
 #include "avc_gemm_variants.h"
 #undef AVC_GEMM_VARIANT
@@ -926,18 +944,18 @@ static hipError_t launch_gemm(const Launch& L, int variant, hipStream_t s) {
     }
     if (L.ksplit > 1) {
         const long groups = (long)L.maxM * cdiv(L.maxN, 4);
-        hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)cdiv((int)groups, 256), 1, L.nprob), dim3(256), 0, s,
-                           L.dprobs, L.ksplit);
+        klaunch(ev, true, splitk_reduce, dim3((unsigned)cdiv((int)groups, 256), 1, L.nprob), dim3(256), 0, s,
+                L.dprobs, L.ksplit);
     }
     return hipGetLastError();
 }
 
-static hipError_t launch_one(const Launch& L, hipStream_t s) {
+static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nullptr) {
     switch (L.kind) {
     case L_GEMM:
-        return launch_gemm(L, L.variant, s);
+        return launch_gemm(L, L.variant, s, ev);
     case L_HEAD:
-        hipLaunchKernelGGL(se_head, L.grid, L.block, L.shmem, s, L.head);
+        klaunch(ev, false, se_head, L.grid, L.block, L.shmem, s, L.head);
         return hipGetLastError();
     default:
         return hipErrorInvalidValue;
@@ -949,7 +967,7 @@ static std::string kernel_name(const Launch& L) {
 }
 
 // Time every tile variant of every GEMM launch of `pl` on the ctx stream and keep
-// the fastest (median of 3 after a warm-up).  Runs once per workspace build.
+// the fastest (median of 5 after a warm-up).  Runs once per workspace build.
 // Tune cache (AVC_TUNE_FILE): lines "key variant" so a profiled re-run (rocprofv3)
 // replays the same tile choices without the tuning launches.
 static std::string tune_key(avc_ctx* ctx, const Plan& pl, size_t li) {
@@ -973,7 +991,28 @@ static std::map<std::string, int> read_tune_file() {
     return m;
 }
 
+// AVC_PRINT_PLAN=1: one stderr line per launch of a tuned plan (position, layer,
+// kernel, grid, split-K) -- lets a rocprofv3 trace be read layer by layer.
+static void print_plan(avc_ctx* ctx, const Plan& pl) {
+    if (!getenv("AVC_PRINT_PLAN")) return;
+    const char* tag = &pl == &ctx->ws.fwd ? "fwd" : (&pl == &ctx->ws.iter ? "iter" : "iterbf16");
+    for (size_t i = 0; i < pl.launches.size(); ++i) {
+        const Launch& L = pl.launches[i];
+        const dim3 g = L.kind == L_GEMM ? gemm_grid(L, L.variant) : L.grid;
+        fprintf(stderr, "plan %s %zu %s %s grid=%u,%u,%u ksplit=%d flop=%.4g\n", tag, i, L.name.c_str(),
+                L.kind == L_GEMM ? VARIANTS[L.variant].name : L.name.c_str(), g.x, g.y, g.z,
+                L.ksplit, L.flop);
+    }
+}
+
+static int autotune_(avc_ctx* ctx, Plan& pl);
 static int autotune(avc_ctx* ctx, Plan& pl) {
+    const int rc = autotune_(ctx, pl);
+    if (!rc) print_plan(ctx, pl);
+    return rc;
+}
+
+static int autotune_(avc_ctx* ctx, Plan& pl) {
     const char* env = getenv("AVC_AUTOTUNE");
     if (env && env[0] == '0') return 0;
     std::map<std::string, int> cache = read_tune_file();
@@ -999,18 +1038,18 @@ static int autotune(avc_ctx* ctx, Plan& pl) {
         float best_ms = 1e30f;
         for (int v = 0; v < NVARIANTS; ++v) {
             if (!variant_fits(L, v)) continue;
-            float t[3];
+            float t[5];
             HIPCHK(launch_gemm(L, v, ctx->stream));
-            for (int r = 0; r < 3; ++r) {
+            for (int r = 0; r < 5; ++r) {
                 HIPCHK(hipEventRecord(a, ctx->stream));
                 HIPCHK(launch_gemm(L, v, ctx->stream));
                 HIPCHK(hipEventRecord(b, ctx->stream));
                 HIPCHK(hipEventSynchronize(b));
                 HIPCHK(hipEventElapsedTime(&t[r], a, b));
             }
-            std::sort(t, t + 3);
-            if (t[1] < best_ms) {
-                best_ms = t[1];
+            std::sort(t, t + 5);
+            if (t[2] < best_ms) {
+                best_ms = t[2];
                 best = v;
             }
         }
@@ -1029,37 +1068,34 @@ static int autotune(avc_ctx* ctx, Plan& pl) {
     return 0;
 }
 
+static void prof_add(avc_ctx* ctx, const std::string& nm, float ms, double flop) {
+    auto& s = ctx->prof[nm];
+    s.first += ms;
+    s.second += flop;
+    ctx->prof_n[nm] += 1;
+}
+
 static int run_plan(avc_ctx* ctx, const Plan& pl, bool prof) {
+    KEv ev;
+    if (prof)
+        for (hipEvent_t* e : {&ev.gemm0, &ev.gemm1, &ev.red0, &ev.red1}) HIPCHK(hipEventCreate(e));
     for (const Launch& L : pl.launches) {
-        hipEvent_t a = nullptr, b = nullptr;
-        if (prof) {
-            HIPCHK(hipEventCreate(&a));
-            HIPCHK(hipEventCreate(&b));
-            HIPCHK(hipEventRecord(a, ctx->stream));
-        }
-        hipError_t e = launch_one(L, ctx->stream);
+        hipError_t e = launch_one(L, ctx->stream, prof ? &ev : nullptr);
         if (e != hipSuccess) return fail("launch %s: %s", kernel_name(L).c_str(), hipGetErrorString(e));
-        if (prof) {
-            HIPCHK(hipEventRecord(b, ctx->stream));
-            HIPCHK(hipEventSynchronize(b));
-            float ms = 0;
-            HIPCHK(hipEventElapsedTime(&ms, a, b));
-            const std::string nm = kernel_name(L);
-            auto& s = ctx->prof[nm];
-            s.first += ms;
-            s.second += L.flop;
-            ctx->prof_n[nm] += 1;
-            if (getenv("AVC_PROFILE_ROLES")) {   // per-layer breakdown (diagnostics)
-                const std::string rn = "role:" + L.name + "|" + nm;
-                auto& r = ctx->prof[rn];
-                r.first += ms;
-                r.second += L.flop;
-                ctx->prof_n[rn] += 1;
-            }
-            hipEventDestroy(a);
-            hipEventDestroy(b);
-        }
+        if (!prof) continue;
+        const bool red = L.kind == L_GEMM && L.ksplit > 1;
+        HIPCHK(hipEventSynchronize(red ? ev.red1 : ev.gemm1));
+        float ms = 0, ms_red = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ev.gemm0, ev.gemm1));
+        if (red) HIPCHK(hipEventElapsedTime(&ms_red, ev.red0, ev.red1));
+        const std::string nm = kernel_name(L);
+        prof_add(ctx, nm, ms, L.flop);
+        if (red) prof_add(ctx, "splitk_reduce", ms_red, 0.0);
+        if (getenv("AVC_PROFILE_ROLES"))   // per-layer breakdown (diagnostics), reduce included
+            prof_add(ctx, "role:" + L.name + "|" + nm, ms + ms_red, L.flop);
     }
+    if (prof)
+        for (hipEvent_t e : {ev.gemm0, ev.gemm1, ev.red0, ev.red1}) (void)hipEventDestroy(e);
     return 0;
 }
 

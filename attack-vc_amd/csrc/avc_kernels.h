@@ -11,6 +11,7 @@ constexpr int KSEG = 64;        // K-segment granule: a segment's rows are padde
                                 // (32 or 64 rows) ever straddles two segments
 constexpr int KALIGN = 64;      // A matrices carry zero rows up to a multiple of the largest K chunk
 constexpr int MAX_SEGS = 8;
+constexpr int KSPLIT_MAX = 4;    // largest split-K factor (slab planes)
 
 // How the im2col B-operand rows of one K segment are gathered from HBM.
 enum Prec : int32_t { PREC_F32 = 0, PREC_BF16 = 1 };

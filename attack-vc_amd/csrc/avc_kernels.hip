@@ -241,13 +241,25 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
     }
     // d/d hN of the mean over time, and its copy gated by the ReLU that produced h_N
     const int TN = A.TN;
+    // (mask loads of 4 elements issued before their stores: no serialised latency)
     for (int u = 0; u < HU && u0 + u < A.B; ++u) {
         const size_t off = (size_t)(u0 + u) * C * TN;
-        for (int idx = tid; idx < C * TN; idx += blockDim.x) {
-            const int c = idx / TN;
-            const float g = GB[c * HU + u] / (float)TN;
-            A.g_hN[off + idx] = g;
-            A.g_hN_masked[off + idx] = g * act_d(A.mask_hN[off + idx], A.act);
+        for (int i0 = tid; i0 < C * TN; i0 += 4 * (int)blockDim.x) {
+            float mk[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int idx = i0 + q * blockDim.x;
+                mk[q] = idx < C * TN ? A.mask_hN[off + idx] : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int idx = i0 + q * blockDim.x;
+                if (idx < C * TN) {
+                    const float g = GB[(idx / TN) * HU + u] / (float)TN;
+                    A.g_hN[off + idx] = g;
+                    A.g_hN_masked[off + idx] = g * act_d(mk[q], A.act);
+                }
+            }
         }
     }
 }
