@@ -19,6 +19,7 @@ MAX_BLOCKS = 16
 
 PREC = {"fp32": 0, "bf16": 1}
 REDUCE = {"independent": 0, "mean": 1}
+ENGINE = {"auto": 0, "layered": 1, "fused": 2}
 
 
 class SECfg(ctypes.Structure):
@@ -49,6 +50,8 @@ SIGNATURES = [
     ("avc_emb_attack", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_set_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("avc_get_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_get_profile", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_double)]),
@@ -161,6 +164,13 @@ class Context:
                                         B, T, float(eps), int(n_iters), ctypes.c_void_p(out.data_ptr()),
                                         ctypes.byref(o), ctypes.c_void_p(stream)))
         return out, losses, grad0
+
+    def set_engine(self, engine: str = "auto"):
+        """"auto" | "layered" | "fused" (include/avc.h AVC_ENGINE_*)."""
+        _check(lib().avc_set_engine(self.h, ENGINE[engine]))
+
+    def engine_for(self, T: int) -> str:
+        return {v: k for k, v in ENGINE.items()}[lib().avc_get_engine(self.h, int(T))]
 
     # --- profiling (bench.py roofline) ---------------------------------------------
     def set_profiling(self, on: bool):

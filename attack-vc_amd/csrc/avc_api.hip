@@ -23,7 +23,12 @@ __global__ void splitk_reduce(const Problem* __restrict__ probs, int ksplit);
 __global__ void se_head(HeadArgs A);
 __global__ void attack_init(const float* vc, const float* ptb0, float* ptb, float* m, float* v, float* adv,
                             float eps, size_t n);
+template <int PREC, int STD>
+__global__ void se_fwd_fused(FusedArgs A);
+template <int PREC, int STD>
+__global__ void se_bwd_fused(FusedArgs A);
 }  // namespace avc
+#include "avc_fused_lds.h"
 
 using namespace avc;
 
@@ -63,7 +68,7 @@ struct HostConv {
     const float* b;
 };
 
-enum LaunchKind { L_GEMM, L_HEAD };
+enum LaunchKind { L_GEMM, L_HEAD, L_FZ_FWD, L_FZ_BWD };
 
 // conv_gemm instantiations (avc_gemm_variants.h); the planner autotunes one per
 // launch and precision on first use of a workspace.
@@ -94,6 +99,8 @@ struct Launch {
     Problem* dprobs = nullptr;   // device problem table (L_GEMM*)
     int nprob = 0;
     HeadArgs head{};
+    FusedArgs fz{};              // L_FZ_*: per-utterance fused SpeakerEncoder pass (prec = PREC_*)
+    int fz_std = 0;              // L_FZ_*: compile-time-shaped instantiation (standard config, T = 128)
     double flop = 0;             // algorithmic FLOPs of this launch
     std::string name;
 };
@@ -109,6 +116,10 @@ struct Workspace {
     DevBuf xin, adv, vc, ptb, m, v, bank, h0, gbank, gxd, g1, ghx, ghy, gmx, gmy, emb_fwd, org, tgt, grad0;
     std::vector<DevBuf> a1, a2, hb;   // per block
     DevBuf losses, table, scal, slab;
+    DevBuf pooled, gpooled;           // fused path: [B][128] time-mean of h_N and its gradient
+    unsigned long long* masks = nullptr;   // fused path: ReLU' ballot words [B][mask_words]
+    int mask_words = 0;
+    bool fused = false;               // this (B, T) runs on the fused engine
     int iters_cap = 0;
     int* step = nullptr;
     Plan fwd, iter, iter_bf16;
@@ -133,6 +144,10 @@ struct avc_ctx {
     DevBuf bias_in;
     std::vector<DevBuf> bias_c1, bias_c2;
     DevBuf head_Wp, head_WpT, head_bias;
+    bool fused_ok = false;              // config fits the fused per-utterance engine
+    int engine = AVC_ENGINE_AUTO;       // avc_set_engine
+    std::vector<DevBuf> fz_bufs;        // packed fused-engine A operands (both precisions)
+    FusedW fzw[2];                      // [PREC_F32], [PREC_BF16]
     std::map<const float*, void*> bf16_of;   // fp32 A matrix -> its bf16 copy (device)
     hipStream_t stream = nullptr;
     hipEvent_t ev_user = nullptr, ev_done = nullptr;
@@ -273,6 +288,101 @@ static int validate_cfg(const avc_se_cfg& c) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------------
+// fused per-utterance engine: eligibility and A-operand packing (avc_fused.hip)
+// ---------------------------------------------------------------------------------
+static bool fused_cfg_ok(const avc_se_cfg& c) {
+    if (c.c_in != FZ_CIN || c.c_h != FZ_C || c.c_bank != FZ_C || c.c_out > 128 || c.c_out % 16) return false;
+    if (c.bank_scale != 1 || c.bank_size < 1 || c.bank_size > FZ_MAXNB) return false;
+    if (c.kernel_size % 2 == 0 || c.kernel_size > 5) return false;   // dY images carry 2*(ks/2) <= 4 zero rows
+    if (c.n_conv_blocks < 1 || c.n_conv_blocks > FZ_MAXBLK) return false;
+    for (int l = 0; l < c.n_conv_blocks; ++l)
+        if (c.subsample[l] != 1 && c.subsample[l] != 2) return false;
+    return true;
+}
+
+// Fragment packing: [16-row tile][K step][lane][VE] with lane (r = l&15, q = l>>4)
+// holding A[16 mt + r][KS step + VE q + e]; zero outside [M) x [K).
+template <typename G>
+static int fz_pack(avc_ctx* ctx, int prec, int M, int K, G get, const void*& dst) {
+    const int KS = prec == PREC_F32 ? 16 : 32, VE = KS / 4;
+    const int nmt = cdiv(M, 16), nst = cdiv(K, KS);
+    std::vector<float> v((size_t)nmt * nst * 64 * VE, 0.f);
+    for (int mt = 0; mt < nmt; ++mt)
+        for (int ps = 0; ps < nst; ++ps)
+            for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < VE; ++e) {
+                    const int m = 16 * mt + (l & 15), k = KS * ps + VE * (l >> 4) + e;
+                    if (m < M && k < K) v[(((size_t)mt * nst + ps) * 64 + l) * VE + e] = get(m, k);
+                }
+    ctx->fz_bufs.emplace_back();
+    DevBuf& b = ctx->fz_bufs.back();
+    if (prec == PREC_F32) {
+        if (upload(b, v)) return 1;
+    } else {
+        std::vector<uint16_t> h(v.size());
+        for (size_t i = 0; i < v.size(); ++i) h[i] = to_bf16(v[i]);
+        HIPCHK(hipMalloc(&b.p, h.size() * 2));
+        b.n = h.size() / 2;
+        HIPCHK(hipMemcpy(b.p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    }
+    dst = b.p;
+    return 0;
+}
+
+static int pack_fused(avc_ctx* ctx, const std::vector<HostConv>& bank, const HostConv& inc,
+                      const std::vector<HostConv>& c1, const std::vector<HostConv>& c2) {
+    const avc_se_cfg& c = ctx->cfg;
+    const int nb = ctx->nb, C = FZ_C, CI = FZ_CIN, ks = c.kernel_size, cat = inc.ci;
+    ctx->fz_bufs.reserve(2 * (4 * nb + 2 + 4 * c.n_conv_blocks));
+    for (int prec = 0; prec < 2; ++prec) {
+        FusedW& W = ctx->fzw[prec];
+        int rc = 0;
+        for (int kb = 0; kb < nb; ++kb) {
+            const HostConv& q = bank[kb];
+            const int k = q.k;
+            // forward bank: A[co][j*80 + ci] = W[co][ci][j]
+            rc |= fz_pack(ctx, prec, C, k * CI, [&](int m, int kk) { return q.W[((size_t)m * CI + kk % CI) * k + kk / CI]; },
+                          W.bank[kb]);
+            // in_conv, bank block kb: A[co][ci'] = W_in[co][kb*128 + ci']
+            rc |= fz_pack(ctx, prec, C, C, [&](int m, int kk) { return inc.W[(size_t)m * cat + kb * C + kk]; }, W.in_b[kb]);
+            // in_conv^T, bank block: A[ci'][co] = W_in[co][kb*128 + ci']
+            rc |= fz_pack(ctx, prec, C, C, [&](int m, int kk) { return inc.W[(size_t)kk * cat + kb * C + m]; }, W.inT_b[kb]);
+            // bank^T: A[ci][j*128 + co] = W[co][ci][j]
+            rc |= fz_pack(ctx, prec, CI, k * C, [&](int m, int kk) { return q.W[((size_t)(kk % C) * CI + m) * k + kk / C]; },
+                          W.bankT[kb]);
+            W.b_bank[kb] = ctx->bias_bank[kb].p;
+        }
+        rc |= fz_pack(ctx, prec, C, CI, [&](int m, int kk) { return inc.W[(size_t)m * cat + nb * C + kk]; }, W.in_x);
+        rc |= fz_pack(ctx, prec, CI, C, [&](int m, int kk) { return inc.W[(size_t)kk * cat + nb * C + m]; }, W.inT_x);
+        W.b_in = ctx->bias_in.p;
+        for (int l = 0; l < c.n_conv_blocks; ++l) {
+            for (int which = 0; which < 2; ++which) {
+                const HostConv& q = which ? c2[l] : c1[l];
+                const void*& f = which ? W.c2[l] : W.c1[l];
+                const void*& t = which ? W.c2T[l] : W.c1T[l];
+                rc |= fz_pack(ctx, prec, C, ks * C, [&](int m, int kk) { return q.W[((size_t)m * C + kk % C) * ks + kk / C]; }, f);
+                rc |= fz_pack(ctx, prec, C, ks * C, [&](int m, int kk) { return q.W[((size_t)(kk % C) * C + m) * ks + kk / C]; }, t);
+            }
+            W.b_c1[l] = ctx->bias_c1[l].p;
+            W.b_c2[l] = ctx->bias_c2[l].p;
+        }
+        if (rc) return 1;
+    }
+    // every fused kernel needs more than the default 64 KiB of dynamic LDS
+    const std::pair<const void*, int> fns[] = {
+        {(const void*)se_fwd_fused<PREC_F32, 0>, fz_lds_fwd(PREC_F32, 128, 5)},
+        {(const void*)se_fwd_fused<PREC_BF16, 0>, fz_lds_fwd(PREC_BF16, 128, 5)},
+        {(const void*)se_bwd_fused<PREC_F32, 0>, fz_lds_bwd(PREC_F32, 128)},
+        {(const void*)se_bwd_fused<PREC_BF16, 0>, fz_lds_bwd(PREC_BF16, 128)},
+        {(const void*)se_fwd_fused<PREC_F32, 1>, fz_lds_fwd(PREC_F32, 128, 5)},
+        {(const void*)se_fwd_fused<PREC_BF16, 1>, fz_lds_fwd(PREC_BF16, 128, 5)},
+        {(const void*)se_bwd_fused<PREC_F32, 1>, fz_lds_bwd(PREC_F32, 128)},
+        {(const void*)se_bwd_fused<PREC_BF16, 1>, fz_lds_bwd(PREC_BF16, 128)}};
+    for (auto& fn : fns) HIPCHK(hipFuncSetAttribute(fn.first, hipFuncAttributeMaxDynamicSharedMemorySize, fn.second));
+    return 0;
+}
+
 extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, size_t n_weights, avc_ctx** out) {
     if (!cfgp || !w || !out) return fail("avc_create: null argument");
     const avc_se_cfg& c = *cfgp;
@@ -410,6 +520,8 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
         up(ctx->head_WpT, WpT);
         up(ctx->head_bias, bias);
     }
+    ctx->fused_ok = fused_cfg_ok(c);
+    if (!rc && ctx->fused_ok) rc |= pack_fused(ctx, bank, inc, c1, c2);
     if (rc) {
         avc_destroy(ctx);
         return 1;
@@ -448,7 +560,7 @@ static void free_plans(Workspace& ws) {
 static void free_ws(Workspace& ws) {
     free_plans(ws);
     DevBuf* bufs[] = {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.bank, &ws.h0, &ws.gbank, &ws.gxd,
-                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal, &ws.slab};
+                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal, &ws.slab, &ws.pooled, &ws.gpooled};
     for (DevBuf* b : bufs) dfree(*b);
     for (auto& b : ws.a1) dfree(b);
     for (auto& b : ws.a2) dfree(b);
@@ -458,6 +570,9 @@ static void free_ws(Workspace& ws) {
     ws.hb.clear();
     if (ws.step) hipFree(ws.step);
     ws.step = nullptr;
+    if (ws.masks) hipFree(ws.masks);
+    ws.masks = nullptr;
+    ws.fused = false;
     ws.built = false;
     ws.B = ws.T = 0;
     ws.iters_cap = 0;
@@ -474,6 +589,7 @@ extern "C" void avc_destroy(avc_ctx* ctx) {
     for (DevBuf* b : {&ctx->AtF_in, &ctx->AtB_in, &ctx->AtB_bank, &ctx->bias_in, &ctx->head_Wp,
                       &ctx->head_WpT, &ctx->head_bias})
         dfree(*b);
+    for (auto& b : ctx->fz_bufs) dfree(b);
     for (auto& kv : ctx->bf16_of) (void)hipFree(kv.second);
     ctx->bf16_of.clear();
     if (ctx->ev_user) hipEventDestroy(ctx->ev_user);
@@ -818,7 +934,148 @@ static int plan_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------------
+// fused per-utterance plans: [se_fwd_fused] -> se_head (batched) [-> se_bwd_fused]
+// ---------------------------------------------------------------------------------
+static double fz_fwd_flop(const avc_se_cfg& c, const std::vector<int>& Tl, const std::vector<int>& bank_k) {
+    double mac = 0;
+    const int T = Tl[0];
+    for (int k : bank_k) mac += (double)c.c_bank * c.c_in * k * T;
+    mac += (double)c.c_h * (c.c_bank * (int)bank_k.size() + c.c_in) * T;
+    for (int l = 0; l < c.n_conv_blocks; ++l)
+        mac += (double)c.c_h * c.c_h * c.kernel_size * (Tl[l] + Tl[l + 1]);
+    return 2.0 * mac;
+}
+
+static FusedArgs fused_args(avc_ctx* ctx, Workspace& ws, int prec) {
+    const avc_se_cfg& c = ctx->cfg;
+    FusedArgs A{};
+    A.B = ws.B;
+    A.T = ws.T;
+    A.nb = ctx->nb;
+    A.ks = c.kernel_size;
+    A.nblk = c.n_conv_blocks;
+    A.act = c.act;
+    for (int l = 0; l < c.n_conv_blocks; ++l) A.sub[l] = c.subsample[l];
+    for (int l = 0; l <= c.n_conv_blocks; ++l) A.Tl[l] = ws.Tl[l];
+    A.mask_words = ws.mask_words;
+    A.masks = ws.masks;
+    A.pooled = ws.pooled.p;
+    A.g_pooled = ws.gpooled.p;
+    A.step = ws.step;
+    A.scal = ws.scal.p;
+    A.table_len = ws.iters_cap;
+    A.w = ctx->fzw[prec];
+    return A;
+}
+
+// the compile-time-shaped kernels: AdaIN-VC config.yaml defaults at T = 128
+static bool fused_std(avc_ctx* ctx, int T) {
+    const avc_se_cfg& c = ctx->cfg;
+    if (T != 128 || ctx->nb != 8 || c.kernel_size != 5 || c.n_conv_blocks != 6) return false;
+    for (int l = 0; l < 6; ++l)
+        if (c.subsample[l] != ((l & 1) ? 2 : 1)) return false;
+    const char* e = getenv("AVC_FUSED_STD");
+    return !(e && e[0] == '0');
+}
+
+static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, bool attack, int prec) {
+    const avc_se_cfg& c = ctx->cfg;
+    const int B = ws.B;
+    {
+        Launch L;
+        L.kind = L_FZ_FWD;
+        L.prec = prec;
+        L.grid = dim3(B);
+        L.block = dim3(256);
+        L.shmem = fz_lds_fwd(prec, ws.T, c.kernel_size);
+        L.fz = fused_args(ctx, ws, prec);
+        L.fz.x = x;
+        L.fz.write_masks = attack ? 1 : 0;
+        L.fz.tick = attack ? ws.step : nullptr;
+        L.fz_std = fused_std(ctx, ws.T);
+        L.flop = fz_fwd_flop(c, ws.Tl, ctx->bank_k) * B;
+        L.name = prec == PREC_F32 ? "se_fwd_fused<f32>" : "se_fwd_fused<bf16>";
+        pl.launches.push_back(L);
+    }
+    {
+        Launch L;
+        L.kind = L_HEAD;
+        L.grid = dim3(cdiv(B, 16));
+        L.block = dim3(512);
+        const int S = std::max(c.c_h, c.c_out);
+        L.shmem = (size_t)(2 * c.n_dense_blocks + 5) * S * 16 * sizeof(float);
+        HeadArgs& A = L.head;
+        A.pooled_in = ws.pooled.p;
+        A.g_pooled = attack ? ws.gpooled.p : nullptr;
+        A.Wp = ctx->head_Wp.p;
+        A.WpT = ctx->head_WpT.p;
+        A.bias = ctx->head_bias.p;
+        A.emb_out = ws.emb_fwd.p;
+        A.tgt = ws.tgt.p;
+        A.org = ws.org.p;
+        A.losses = ws.losses.p;
+        A.step = ws.step;
+        A.B = B;
+        A.C = c.c_h;
+        A.TN = ws.Tl[c.n_conv_blocks];
+        A.D = c.c_out;
+        A.n_dense = c.n_dense_blocks;
+        A.act = c.act;
+        A.mode = attack ? 1 : 0;
+        A.scal = ws.scal.p;
+        A.loss_len = ws.iters_cap;
+        const double dense = 2.0 * c.c_h * c.c_h * 2 * c.n_dense_blocks + 2.0 * c.c_out * c.c_h;
+        L.flop = dense * B * (attack ? 2 : 1);
+        L.name = "se_head";
+        pl.launches.push_back(L);
+    }
+    return 0;
+}
+
+static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) {
+    Launch L;
+    L.kind = L_FZ_BWD;
+    L.prec = prec;
+    L.grid = dim3(ws.B);
+    L.block = dim3(256);
+    L.shmem = fz_lds_bwd(prec, ws.T);
+    L.fz = fused_args(ctx, ws, prec);
+    L.fz_std = fused_std(ctx, ws.T);
+    AdamArgs& A = L.fz.adam;
+    A.ptb = ws.ptb.p;
+    A.m = ws.m.p;
+    A.v = ws.v.p;
+    A.vc = ws.vc.p;
+    A.adv = ws.adv.p;
+    A.table = ws.table.p;
+    A.grad0 = ws.grad0.p;
+    A.b1c = (float)(1.0 - 0.9);
+    A.b2 = 0.999f;
+    A.b2c = (float)(1.0 - 0.999);
+    A.adam_eps = 1e-8f;
+    L.flop = fz_fwd_flop(ctx->cfg, ws.Tl, ctx->bank_k) * ws.B;   // input-gradient only
+    L.name = prec == PREC_F32 ? "se_bwd_fused<f32>" : "se_bwd_fused<bf16>";
+    pl.launches.push_back(L);
+    return 0;
+}
+
+static int plan_iteration(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) {
+    if (ws.fused)
+        return plan_fused_forward(ctx, ws, pl, ws.adv.p, true, prec) || plan_fused_backward(ctx, ws, pl, prec);
+    return plan_forward(ctx, ws, pl, ws.adv.p, true, prec) || plan_backward(ctx, ws, pl, prec);
+}
+
 static int autotune(avc_ctx* ctx, Plan& pl);
+
+// fused per-utterance engine for this T?  (AVC_FUSED=0 in the environment forces the
+// layered engine for A/B runs)
+static bool want_fused(avc_ctx* ctx, int T) {
+    if (ctx->engine == AVC_ENGINE_LAYERED) return false;
+    const char* fe = getenv("AVC_FUSED");
+    if (ctx->engine == AVC_ENGINE_AUTO && fe && fe[0] == '0') return false;
+    return ctx->fused_ok && T <= 128;
+}
 
 static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     Workspace& ws = ctx->ws;
@@ -845,7 +1102,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         if (To != Tp) return fail("conv/pool length mismatch at block %d (%d vs %d)", l, To, Tp);
         Tl.push_back(To);
     }
-    const bool same = ws.built && ws.B == B && ws.T == T;
+    const bool same = ws.built && ws.B == B && ws.T == T && ws.fused == want_fused(ctx, T);
     if (same && n_iters <= ws.iters_cap) return 0;
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (!same) {
@@ -855,24 +1112,33 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         ws.Tl = Tl;
         const int nb = ctx->nb;
         const size_t X = (size_t)B * c.c_in * T;
+        ws.fused = want_fused(ctx, T);
         int rc = 0;
-        for (DevBuf* b : {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.gxd, &ws.grad0}) rc |= dalloc(*b, X);
-        rc |= dalloc(ws.bank, (size_t)B * nb * c.c_bank * T);
-        rc |= dalloc(ws.gbank, (size_t)B * nb * c.c_bank * T);
-        const size_t H = (size_t)B * c.c_h * T;
-        for (DevBuf* b : {&ws.h0, &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy}) rc |= dalloc(*b, H);
+        for (DevBuf* b : {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.grad0}) rc |= dalloc(*b, X);
         for (DevBuf* b : {&ws.emb_fwd, &ws.org, &ws.tgt}) rc |= dalloc(*b, (size_t)B * c.c_out);
-        ws.a1.resize(c.n_conv_blocks);
-        ws.a2.resize(c.n_conv_blocks);
-        ws.hb.resize(c.n_conv_blocks);
-        for (int l = 0; l < c.n_conv_blocks; ++l) {
-            rc |= dalloc(ws.a1[l], (size_t)B * c.c_h * Tl[l]);
-            rc |= dalloc(ws.a2[l], (size_t)B * c.c_h * Tl[l + 1]);
-            rc |= dalloc(ws.hb[l], (size_t)B * c.c_h * Tl[l + 1]);
+        if (ws.fused) {
+            ws.mask_words = (nb + 1 + 2 * c.n_conv_blocks) * FZ_MASK_WORDS_PER_LAYER;
+            rc |= dalloc(ws.pooled, (size_t)B * FZ_C);
+            rc |= dalloc(ws.gpooled, (size_t)B * FZ_C);
+            HIPCHK(hipMalloc(&ws.masks, (size_t)B * ws.mask_words * sizeof(unsigned long long)));
+        } else {
+            rc |= dalloc(ws.gxd, X);
+            rc |= dalloc(ws.bank, (size_t)B * nb * c.c_bank * T);
+            rc |= dalloc(ws.gbank, (size_t)B * nb * c.c_bank * T);
+            const size_t H = (size_t)B * c.c_h * T;
+            for (DevBuf* b : {&ws.h0, &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy}) rc |= dalloc(*b, H);
+            ws.a1.resize(c.n_conv_blocks);
+            ws.a2.resize(c.n_conv_blocks);
+            ws.hb.resize(c.n_conv_blocks);
+            for (int l = 0; l < c.n_conv_blocks; ++l) {
+                rc |= dalloc(ws.a1[l], (size_t)B * c.c_h * Tl[l]);
+                rc |= dalloc(ws.a2[l], (size_t)B * c.c_h * Tl[l + 1]);
+                rc |= dalloc(ws.hb[l], (size_t)B * c.c_h * Tl[l + 1]);
+            }
+            rc |= dalloc(ws.slab, (size_t)KSPLIT_MAX * std::max(c.c_h, c.c_in) * B * T);
         }
         HIPCHK(hipMalloc(&ws.step, sizeof(int)));
         rc |= dalloc(ws.scal, 4);
-        rc |= dalloc(ws.slab, (size_t)KSPLIT_MAX * std::max(c.c_h, c.c_in) * B * T);
         if (rc) return 1;
     }
     const int cap = std::max(n_iters, std::max(ws.iters_cap, 1));
@@ -881,9 +1147,12 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     ws.iters_cap = cap;
     // (re)build plans: pointers may have moved (the bf16 plan is rebuilt on demand)
     free_plans(ws);
-    if (plan_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return 1;
-    if (plan_forward(ctx, ws, ws.iter, ws.adv.p, true, PREC_F32)) return 1;
-    if (plan_backward(ctx, ws, ws.iter, PREC_F32)) return 1;
+    if (ws.fused) {
+        if (plan_fused_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return 1;
+    } else {
+        if (plan_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return 1;
+    }
+    if (plan_iteration(ctx, ws, ws.iter, PREC_F32)) return 1;
     // autotune with a valid Adam step (1) and eps/gscale (the kernels clamp anyway)
     const float scal0[4] = {0.1f, 0.f, 0.f, 0.f};
     HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
@@ -957,6 +1226,16 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
     case L_HEAD:
         klaunch(ev, false, se_head, L.grid, L.block, L.shmem, s, L.head);
         return hipGetLastError();
+    case L_FZ_FWD:
+    case L_FZ_BWD: {
+        const bool f = L.kind == L_FZ_FWD;
+        auto k = f ? (L.prec == PREC_F32 ? (L.fz_std ? se_fwd_fused<PREC_F32, 1> : se_fwd_fused<PREC_F32, 0>)
+                                         : (L.fz_std ? se_fwd_fused<PREC_BF16, 1> : se_fwd_fused<PREC_BF16, 0>))
+                   : (L.prec == PREC_F32 ? (L.fz_std ? se_bwd_fused<PREC_F32, 1> : se_bwd_fused<PREC_F32, 0>)
+                                         : (L.fz_std ? se_bwd_fused<PREC_BF16, 1> : se_bwd_fused<PREC_BF16, 0>));
+        klaunch(ev, false, k, L.grid, L.block, L.shmem, s, L.fz);
+        return hipGetLastError();
+    }
     default:
         return hipErrorInvalidValue;
     }
@@ -1127,6 +1406,22 @@ extern "C" int avc_se_forward(avc_ctx* ctx, const float* x, int B, int T, float*
     return end_call(ctx, us);
 }
 
+extern "C" int avc_set_engine(avc_ctx* ctx, int engine) {
+    if (!ctx) return fail("null ctx");
+    if (engine != AVC_ENGINE_AUTO && engine != AVC_ENGINE_LAYERED && engine != AVC_ENGINE_FUSED)
+        return fail("bad engine %d", engine);
+    if (engine == AVC_ENGINE_FUSED && !ctx->fused_ok)
+        return fail("the fused engine needs c_in=80, c_h=c_bank=128, bank_scale=1, bank_size<=8, odd kernel_size<=5, "
+                    "<=8 conv blocks with subsample 1 or 2");
+    ctx->engine = engine;
+    return 0;
+}
+
+extern "C" int avc_get_engine(avc_ctx* ctx, int T) {
+    if (!ctx) return -1;
+    return want_fused(ctx, T) ? AVC_ENGINE_FUSED : AVC_ENGINE_LAYERED;
+}
+
 extern "C" int avc_set_profiling(avc_ctx* ctx, int enable) {
     if (!ctx) return fail("null ctx");
     ctx->profiling = enable != 0;
@@ -1152,8 +1447,7 @@ extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* ad
     Workspace& ws = ctx->ws;
     const bool bf16 = o.precision == AVC_PREC_BF16;
     if (bf16 && ws.iter_bf16.launches.empty()) {
-        if (plan_forward(ctx, ws, ws.iter_bf16, ws.adv.p, true, PREC_BF16)) return 1;
-        if (plan_backward(ctx, ws, ws.iter_bf16, PREC_BF16)) return 1;
+        if (plan_iteration(ctx, ws, ws.iter_bf16, PREC_BF16)) return 1;
         const float scal0[4] = {0.1f, 0.f, 0.f, 0.f};
         HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
         HIPCHK(hipMemset(ws.step, 0, sizeof(int)));

@@ -101,6 +101,58 @@ struct HeadArgs {
     const float* scal;        // [1] = 2 / n_elems of the MSE mean (per call)
     int32_t loss_len;         // rows of `losses` (iterations); writes beyond are dropped
     int32_t B, C, TN, D, n_dense, act, mode;
+    const float* pooled_in;   // fused path: [B][C] time-mean of h_N (replaces the hN pooling)
+    float* g_pooled;          // fused path: [B][C] d loss / d pooled (replaces the g_hN expansion)
+};
+
+// ---------------------------------------------------------------------------------
+// Fused per-utterance SpeakerEncoder engine (avc_fused.hip): one workgroup of 4
+// waves owns one utterance; every activation of the conv stack stays in LDS.
+// Wave w owns output channels [32w, 32w+32) of every 128-channel layer.
+// ---------------------------------------------------------------------------------
+constexpr int FZ_MAXNB = 8;       // bank kernels
+constexpr int FZ_MAXBLK = 8;      // conv blocks
+constexpr int FZ_MAXNF = 9;       // 16-column fragments per layer (T <= 128, + edge columns)
+constexpr int FZ_CIN = 80;        // mel bins (the only c_in the fused path is built for)
+constexpr int FZ_C = 128;         // c_h == c_bank == c_out
+constexpr int FZ_MASK_WORDS_PER_LAYER = 4 * 2 * FZ_MAXNF * 4;   // u64 ballot words (4 waves)
+
+// Packed A operands: [m_tile(16 rows)][k_step][64 lanes][16 bytes]; lane (r = l&15,
+// q = l>>4) holds A[16*mt + r][KS*step + VE*q + e], e < VE (VE = 4 fp32 / 8 bf16, KS = 4*VE).
+// The K index of a conv is (tap j, input channel c) -> j*Cin + c.
+struct FusedW {
+    const void* bank[FZ_MAXNB];       // fwd: M=128, K=k*80
+    const void* in_b[FZ_MAXNB];       // fwd in_conv, bank block kb: M=128, K=128
+    const void* in_x;                 // fwd in_conv, x block: M=128, K=80
+    const void* c1[FZ_MAXBLK];        // fwd conv1: M=128, K=ks*128
+    const void* c2[FZ_MAXBLK];
+    const void* c1T[FZ_MAXBLK];       // dgrad: A[ci][j*128+co] = W[co][ci][j]
+    const void* c2T[FZ_MAXBLK];
+    const void* inT_b[FZ_MAXNB];      // in_conv^T, bank block: A[ci'][co] = W_in[co][kb*128+ci']
+    const void* inT_x;                // in_conv^T, x block: M=80, K=128
+    const void* bankT[FZ_MAXNB];      // bank^T: M=80, K=k*128
+    const float* b_bank[FZ_MAXNB];
+    const float* b_in;
+    const float* b_c1[FZ_MAXBLK];
+    const float* b_c2[FZ_MAXBLK];
+};
+
+struct FusedArgs {
+    int32_t B, T, nb, ks, nblk, act;
+    int32_t sub[FZ_MAXBLK];
+    int32_t Tl[FZ_MAXBLK + 1];
+    int32_t mask_words;               // u64 words per utterance
+    int32_t write_masks;              // fwd: store ReLU' ballot masks (attack iterations)
+    const float* x;                   // fwd input [B][80][T]
+    float* pooled;                    // fwd output [B][128]: mean over T of h_N
+    unsigned long long* masks;        // [B][mask_words]
+    const float* g_pooled;            // bwd input [B][128]
+    int32_t* tick;                    // fwd: block 0 advances the Adam step counter
+    const int32_t* step;              // bwd: Adam step (1-based)
+    const float* scal;                // [0] = attack eps
+    int32_t table_len, pad_;
+    AdamArgs adam;                    // bwd: Adam update + next adv
+    FusedW w;
 };
 
 }  // namespace avc

@@ -108,7 +108,15 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
     }
 
     // AdaptiveAvgPool1d(1) (models.py:275,340): a row's loads all in flight at once
-    for (int idx = tid; idx < C * HU; idx += blockDim.x) {
+    // (the fused engine hands over the time-mean itself)
+    if (A.pooled_in) {
+        for (int idx = tid; idx < C * HU; idx += blockDim.x) {
+            const int u = idx / C, c = idx - u * C;
+            const int b = u0 + u;
+            E[c * HU + u] = b < A.B ? A.pooled_in[(size_t)b * C + c] : 0.f;
+        }
+    }
+    for (int idx = tid; idx < C * HU && !A.pooled_in; idx += blockDim.x) {
         const int u = idx / C, c = idx - u * C;
         const int b = u0 + u;
         float s = 0.f;
@@ -236,6 +244,14 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
             const int u = idx / D, d = idx - u * D;
             const int b = u0 + u;
             if (b < A.B) A.emb_out[(size_t)b * D + d] = EMB[d * HU + u];
+        }
+        return;
+    }
+    if (A.g_pooled) {   // fused engine: d loss / d (time-mean of h_N)
+        for (int idx = tid; idx < C * HU; idx += blockDim.x) {
+            const int u = idx / C, c = idx - u * C;
+            const int b = u0 + u;
+            if (b < A.B) A.g_pooled[(size_t)b * C + c] = GB[c * HU + u];
         }
         return;
     }

@@ -91,6 +91,19 @@ int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, cons
                    int B, int T, float eps, int n_iters, float* out_adv,
                    const avc_attack_opts* opts, void* stream);
 
+/* Compute engine of a context.
+ *  AUTO    (default): FUSED when the config and T allow it, else LAYERED.
+ *  LAYERED: one implicit-GEMM launch per Conv1d / dgrad over the whole batch, activations in HBM
+ *           (any SpeakerEncoder config, any T).
+ *  FUSED  : one workgroup per utterance runs the whole conv stack out of LDS (3 launches per
+ *           iteration); needs c_in=80, c_h=c_bank=128, bank_scale=1, bank_size<=8, odd
+ *           kernel_size<=5, <=8 conv blocks with subsample 1|2, and T<=128 (else LAYERED).
+ * avc_set_engine fails (non-zero) if FUSED is requested for a config that cannot use it;
+ * avc_get_engine returns the engine a call with T frames would run on. */
+enum { AVC_ENGINE_AUTO = 0, AVC_ENGINE_LAYERED = 1, AVC_ENGINE_FUSED = 2 };
+int avc_set_engine(avc_ctx* ctx, int engine);
+int avc_get_engine(avc_ctx* ctx, int T);
+
 /* Per-launch HIP-event profiling (bench.py's roofline).  While enabled, the
  * attack loop runs without graph replay and brackets every kernel launch with
  * HIP events on the ctx's stream, accumulating per-kernel-name launch counts,
