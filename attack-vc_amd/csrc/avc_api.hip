@@ -21,11 +21,12 @@ template <int PREC, int WM, int WN, int WGM, int WGN, int KC, int MODE, int STRI
 __global__ void conv_gemm(const Problem* __restrict__ probs, int ksplit);
 __global__ void splitk_reduce(const Problem* __restrict__ probs, int ksplit);
 __global__ void se_head(HeadArgs A);
+__global__ void se_head_v(HeadArgs A);
 __global__ void attack_init(const float* vc, const float* ptb0, float* ptb, float* m, float* v, float* adv,
                             float eps, size_t n);
-template <int PREC, int STD>
+template <int PREC, int SH>
 __global__ void se_fwd_fused(FusedArgs A);
-template <int PREC, int STD>
+template <int PREC, int SH>
 __global__ void se_bwd_fused(FusedArgs A);
 }  // namespace avc
 #include "avc_fused_lds.h"
@@ -68,7 +69,7 @@ struct HostConv {
     const float* b;
 };
 
-enum LaunchKind { L_GEMM, L_HEAD, L_FZ_FWD, L_FZ_BWD };
+enum LaunchKind { L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD };
 
 // conv_gemm instantiations (avc_gemm_variants.h); the planner autotunes one per
 // launch and precision on first use of a workspace.
@@ -100,7 +101,7 @@ struct Launch {
     int nprob = 0;
     HeadArgs head{};
     FusedArgs fz{};              // L_FZ_*: per-utterance fused SpeakerEncoder pass (prec = PREC_*)
-    int fz_std = 0;              // L_FZ_*: compile-time-shaped instantiation (standard config, T = 128)
+    int fz_shape = 8;            // L_FZ_*: kernel shape SH (0 = standard config at T = 128, else 1|2|4|8)
     double flop = 0;             // algorithmic FLOPs of this launch
     std::string name;
 };
@@ -144,6 +145,7 @@ struct avc_ctx {
     DevBuf bias_in;
     std::vector<DevBuf> bias_c1, bias_c2;
     DevBuf head_Wp, head_WpT, head_bias;
+    DevBuf head_Wr, head_WrT;           // se_head_v: row-major dense/output weights and transposes
     bool fused_ok = false;              // config fits the fused per-utterance engine
     int engine = AVC_ENGINE_AUTO;       // avc_set_engine
     std::vector<DevBuf> fz_bufs;        // packed fused-engine A operands (both precisions)
@@ -292,7 +294,7 @@ static int validate_cfg(const avc_se_cfg& c) {
 // fused per-utterance engine: eligibility and A-operand packing (avc_fused.hip)
 // ---------------------------------------------------------------------------------
 static bool fused_cfg_ok(const avc_se_cfg& c) {
-    if (c.c_in != FZ_CIN || c.c_h != FZ_C || c.c_bank != FZ_C || c.c_out > 128 || c.c_out % 16) return false;
+    if (c.c_in != FZ_CIN || c.c_h != FZ_C || c.c_bank != FZ_C || c.c_out != FZ_C) return false;
     if (c.bank_scale != 1 || c.bank_size < 1 || c.bank_size > FZ_MAXNB) return false;
     if (c.kernel_size % 2 == 0 || c.kernel_size > 5) return false;   // dY images carry 2*(ks/2) <= 4 zero rows
     if (c.n_conv_blocks < 1 || c.n_conv_blocks > FZ_MAXBLK) return false;
@@ -370,15 +372,14 @@ static int pack_fused(avc_ctx* ctx, const std::vector<HostConv>& bank, const Hos
         if (rc) return 1;
     }
     // every fused kernel needs more than the default 64 KiB of dynamic LDS
-    const std::pair<const void*, int> fns[] = {
-        {(const void*)se_fwd_fused<PREC_F32, 0>, fz_lds_fwd(PREC_F32, 128, 5)},
-        {(const void*)se_fwd_fused<PREC_BF16, 0>, fz_lds_fwd(PREC_BF16, 128, 5)},
-        {(const void*)se_bwd_fused<PREC_F32, 0>, fz_lds_bwd(PREC_F32, 128)},
-        {(const void*)se_bwd_fused<PREC_BF16, 0>, fz_lds_bwd(PREC_BF16, 128)},
-        {(const void*)se_fwd_fused<PREC_F32, 1>, fz_lds_fwd(PREC_F32, 128, 5)},
-        {(const void*)se_fwd_fused<PREC_BF16, 1>, fz_lds_fwd(PREC_BF16, 128, 5)},
-        {(const void*)se_bwd_fused<PREC_F32, 1>, fz_lds_bwd(PREC_F32, 128)},
-        {(const void*)se_bwd_fused<PREC_BF16, 1>, fz_lds_bwd(PREC_BF16, 128)}};
+#define AVC_FZ_FNS(SH)                                                                      \
+    {(const void*)se_fwd_fused<PREC_F32, SH>, fz_lds_fwd(PREC_F32, 128, 5)},                \
+        {(const void*)se_fwd_fused<PREC_BF16, SH>, fz_lds_fwd(PREC_BF16, 128, 5)},          \
+        {(const void*)se_bwd_fused<PREC_F32, SH>, fz_lds_bwd(PREC_F32, 128)},                \
+        {(const void*)se_bwd_fused<PREC_BF16, SH>, fz_lds_bwd(PREC_BF16, 128)}
+    const std::pair<const void*, int> fns[] = {AVC_FZ_FNS(0), AVC_FZ_FNS(1), AVC_FZ_FNS(2), AVC_FZ_FNS(4),
+                                               AVC_FZ_FNS(8)};
+#undef AVC_FZ_FNS
     for (auto& fn : fns) HIPCHK(hipFuncSetAttribute(fn.first, hipFuncAttributeMaxDynamicSharedMemorySize, fn.second));
     return 0;
 }
@@ -519,6 +520,27 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
         up(ctx->head_Wp, Wp);
         up(ctx->head_WpT, WpT);
         up(ctx->head_bias, bias);
+        // se_head_v copies: W_l [C][C] then W_out [D][C] and the transposes W_l^T [C][C],
+        // W_out^T [C][D], each row permuted so that thread slice q's weights
+        // W[m][8i + 2q + e] (i < K/8, e < 2) are the contiguous run [q*K/4, (q+1)*K/4)
+        std::vector<float> Wr(tot), WrT(tot);
+        auto perm = [](int k, int K) {   // natural column k -> position in the permuted row
+            const int i = k / 8, q = (k % 8) / 2, e = k % 2;
+            return q * (K / 4) + 2 * i + e;
+        };
+        for (int l = 0; l < 2 * nd; ++l)
+            for (int r = 0; r < c.c_h; ++r)
+                for (int k = 0; k < c.c_h; ++k) {
+                    Wr[l * CC + (size_t)r * c.c_h + perm(k, c.c_h)] = dW[l][(size_t)r * c.c_h + k];
+                    WrT[l * CC + (size_t)k * c.c_h + perm(r, c.c_h)] = dW[l][(size_t)r * c.c_h + k];
+                }
+        for (int r = 0; r < c.c_out; ++r)
+            for (int k = 0; k < c.c_h; ++k) {
+                Wr[2 * nd * CC + (size_t)r * c.c_h + perm(k, c.c_h)] = oW[(size_t)r * c.c_h + k];
+                WrT[2 * nd * CC + (size_t)k * c.c_out + perm(r, c.c_out)] = oW[(size_t)r * c.c_h + k];
+            }
+        up(ctx->head_Wr, Wr);
+        up(ctx->head_WrT, WrT);
     }
     ctx->fused_ok = fused_cfg_ok(c);
     if (!rc && ctx->fused_ok) rc |= pack_fused(ctx, bank, inc, c1, c2);
@@ -587,7 +609,7 @@ extern "C" void avc_destroy(avc_ctx* ctx) {
                     &ctx->bias_c1, &ctx->bias_c2})
         for (auto& b : *v) dfree(b);
     for (DevBuf* b : {&ctx->AtF_in, &ctx->AtB_in, &ctx->AtB_bank, &ctx->bias_in, &ctx->head_Wp,
-                      &ctx->head_WpT, &ctx->head_bias})
+                      &ctx->head_WpT, &ctx->head_bias, &ctx->head_Wr, &ctx->head_WrT})
         dfree(*b);
     for (auto& b : ctx->fz_bufs) dfree(b);
     for (auto& kv : ctx->bf16_of) (void)hipFree(kv.second);
@@ -969,14 +991,17 @@ static FusedArgs fused_args(avc_ctx* ctx, Workspace& ws, int prec) {
     return A;
 }
 
-// the compile-time-shaped kernels: AdaIN-VC config.yaml defaults at T = 128
-static bool fused_std(avc_ctx* ctx, int T) {
+// fused kernel shape: 0 = AdaIN-VC config.yaml defaults at T = 128 (every layer shape
+// compile-time), else the fragment bound 1|2|4|8 >= ceil(T/16)
+static int fused_shape(avc_ctx* ctx, int T) {
     const avc_se_cfg& c = ctx->cfg;
-    if (T != 128 || ctx->nb != 8 || c.kernel_size != 5 || c.n_conv_blocks != 6) return false;
-    for (int l = 0; l < 6; ++l)
-        if (c.subsample[l] != ((l & 1) ? 2 : 1)) return false;
+    bool std_cfg = T == 128 && ctx->nb == 8 && c.kernel_size == 5 && c.n_conv_blocks == 6;
+    for (int l = 0; std_cfg && l < 6; ++l)
+        if (c.subsample[l] != ((l & 1) ? 2 : 1)) std_cfg = false;
     const char* e = getenv("AVC_FUSED_STD");
-    return !(e && e[0] == '0');
+    if (std_cfg && !(e && e[0] == '0')) return 0;
+    const int nf = cdiv(T, 16);
+    return nf <= 1 ? 1 : nf <= 2 ? 2 : nf <= 4 ? 4 : 8;
 }
 
 static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, bool attack, int prec) {
@@ -993,19 +1018,22 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
         L.fz.x = x;
         L.fz.write_masks = attack ? 1 : 0;
         L.fz.tick = attack ? ws.step : nullptr;
-        L.fz_std = fused_std(ctx, ws.T);
+        L.fz_shape = fused_shape(ctx, ws.T);
         L.flop = fz_fwd_flop(c, ws.Tl, ctx->bank_k) * B;
         L.name = prec == PREC_F32 ? "se_fwd_fused<f32>" : "se_fwd_fused<bf16>";
         pl.launches.push_back(L);
     }
     {
         Launch L;
-        L.kind = L_HEAD;
-        L.grid = dim3(cdiv(B, 16));
+        L.kind = L_HEAD_V;
+        L.grid = dim3(cdiv(B, 2));
         L.block = dim3(512);
         const int S = std::max(c.c_h, c.c_out);
-        L.shmem = (size_t)(2 * c.n_dense_blocks + 5) * S * 16 * sizeof(float);
+        L.shmem = (size_t)(2 * c.n_dense_blocks + 5) * S * 2 * sizeof(float) +
+                  (size_t)(2 * c.n_dense_blocks * c.c_h + c.c_out + 4 * c.c_out + 2) * sizeof(float);
         HeadArgs& A = L.head;
+        A.Wr = ctx->head_Wr.p;
+        A.WrT = ctx->head_WrT.p;
         A.pooled_in = ws.pooled.p;
         A.g_pooled = attack ? ws.gpooled.p : nullptr;
         A.Wp = ctx->head_Wp.p;
@@ -1027,7 +1055,7 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
         A.loss_len = ws.iters_cap;
         const double dense = 2.0 * c.c_h * c.c_h * 2 * c.n_dense_blocks + 2.0 * c.c_out * c.c_h;
         L.flop = dense * B * (attack ? 2 : 1);
-        L.name = "se_head";
+        L.name = "se_head_v";
         pl.launches.push_back(L);
     }
     return 0;
@@ -1041,7 +1069,7 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
     L.block = dim3(256);
     L.shmem = fz_lds_bwd(prec, ws.T);
     L.fz = fused_args(ctx, ws, prec);
-    L.fz_std = fused_std(ctx, ws.T);
+    L.fz_shape = fused_shape(ctx, ws.T);
     AdamArgs& A = L.fz.adam;
     A.ptb = ws.ptb.p;
     A.m = ws.m.p;
@@ -1226,13 +1254,21 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
     case L_HEAD:
         klaunch(ev, false, se_head, L.grid, L.block, L.shmem, s, L.head);
         return hipGetLastError();
+    case L_HEAD_V:
+        klaunch(ev, false, se_head_v, L.grid, L.block, L.shmem, s, L.head);
+        return hipGetLastError();
     case L_FZ_FWD:
     case L_FZ_BWD: {
-        const bool f = L.kind == L_FZ_FWD;
-        auto k = f ? (L.prec == PREC_F32 ? (L.fz_std ? se_fwd_fused<PREC_F32, 1> : se_fwd_fused<PREC_F32, 0>)
-                                         : (L.fz_std ? se_fwd_fused<PREC_BF16, 1> : se_fwd_fused<PREC_BF16, 0>))
-                   : (L.prec == PREC_F32 ? (L.fz_std ? se_bwd_fused<PREC_F32, 1> : se_bwd_fused<PREC_F32, 0>)
-                                         : (L.fz_std ? se_bwd_fused<PREC_BF16, 1> : se_bwd_fused<PREC_BF16, 0>));
+        typedef void (*FzK)(FusedArgs);
+#define AVC_FZ_K(SH)                                                                                  \
+    (L.kind == L_FZ_FWD ? (L.prec == PREC_F32 ? (FzK)se_fwd_fused<PREC_F32, SH> : (FzK)se_fwd_fused<PREC_BF16, SH>) \
+                        : (L.prec == PREC_F32 ? (FzK)se_bwd_fused<PREC_F32, SH> : (FzK)se_bwd_fused<PREC_BF16, SH>))
+        const FzK k = L.fz_shape == 0 ? AVC_FZ_K(0)
+                      : L.fz_shape == 1 ? AVC_FZ_K(1)
+                      : L.fz_shape == 2 ? AVC_FZ_K(2)
+                      : L.fz_shape == 4 ? AVC_FZ_K(4)
+                                        : AVC_FZ_K(8);
+#undef AVC_FZ_K
         klaunch(ev, false, k, L.grid, L.block, L.shmem, s, L.fz);
         return hipGetLastError();
     }
@@ -1411,7 +1447,7 @@ extern "C" int avc_set_engine(avc_ctx* ctx, int engine) {
     if (engine != AVC_ENGINE_AUTO && engine != AVC_ENGINE_LAYERED && engine != AVC_ENGINE_FUSED)
         return fail("bad engine %d", engine);
     if (engine == AVC_ENGINE_FUSED && !ctx->fused_ok)
-        return fail("the fused engine needs c_in=80, c_h=c_bank=128, bank_scale=1, bank_size<=8, odd kernel_size<=5, "
+        return fail("the fused engine needs c_in=80, c_h=c_bank=c_out=128, bank_scale=1, bank_size<=8, odd kernel_size<=5, "
                     "<=8 conv blocks with subsample 1 or 2");
     ctx->engine = engine;
     return 0;

@@ -61,6 +61,10 @@ struct Fz<PREC_BF16> {
 
 extern __shared__ __attribute__((aligned(16))) char fz_lds[];
 
+#ifndef AVC_FZ_ABLATE          // timing experiments only: 1 = no A loads, 2 = no mask bookkeeping
+#define AVC_FZ_ABLATE 0
+#endif
+
 typedef unsigned long long u64;
 
 
@@ -102,22 +106,80 @@ __device__ __forceinline__ void zero_acc(f32x4 (&acc)[MT][NF]) {
         for (int f = 0; f < NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// acc[MT][NF] += A x B over `ns` K steps.
-//   Ap  : packed A at this wave's first M tile, lane offset applied (f32x4 units)
-//   amt : f32x4 units between consecutive M tiles (= steps of the matrix * 64)
-//   B   : LDS base of the operand image; rb[f] = row of tap 0 for this lane's column
-//   step s -> packed step ps = (s >> lg)*spt + soff + (s & msk)  (K-split maps)
-//   DJ  : +1 forward (row = rb + j), -1 adjoint (row = rb - j)
-// Pipeline: A is a static 4-deep register ring (slot u holds step s+u; refilled with
-// step s+4+u right after its MFMAs, so three loads stay in flight and no register is
-// ever copied -- a copy of an in-flight load would wait for it); B fragments are read
-// one step ahead into two alternating register sets.
+// ---------------------------------------------------------------------------------
+// A operands and the cross-GEMM prefetch ring
+// ---------------------------------------------------------------------------------
+// One GEMM's A as seen by this wave: packed base at the wave's first M tile (lane offset
+// applied), mt own tiles amt f32x4 apart, ns K steps with the step map
+// ps = (s >> lg)*spt + soff + (s & msk) (identity, or a K-split over waves).
+struct AOp {
+    const f32x4* p;
+    int amt, mt, ns, lg, msk, spt, soff;
+};
+__device__ __forceinline__ AOp aop(const void* packed, int tile0, int mt, int nst, int ns, int lg = 30, int msk = -1,
+                                   int spt = 0, int soff = 0) {
+    AOp o;
+    o.p = reinterpret_cast<const f32x4*>(packed) + (size_t)tile0 * nst * 64 + (threadIdx.x & 63);
+    o.amt = nst * 64;
+    o.mt = mt;
+    o.ns = ns;
+    o.lg = lg;
+    o.msk = msk;
+    o.spt = spt;
+    o.soff = soff;
+    return o;
+}
+__device__ __forceinline__ const f32x4* a_step(const AOp& o, int s) {
+    s = s < o.ns ? s : o.ns - 1;
+    return o.p + (size_t)((s >> o.lg) * o.spt + o.soff + (s & o.msk)) * 64;
+}
+// Four K steps of A in flight: slot u of the ring holds step s+u.  A GEMM refills a slot
+// right after using it, and the refills that run past its last step fetch the NEXT
+// GEMM's first steps instead, so no GEMM starts with an exposed L2/MALL round trip.
+template <int MTR>
+struct ARing {
+    f32x4 a[4][MTR];
+};
+// slot <- step s of A (s < A.ns) or step s - A.ns of N; branch-free (uniform selects);
+// tiles beyond an operand's own count re-read its last tile (an L1 hit, never used)
+template <int MTR>
+__device__ __forceinline__ void ring_load(f32x4 (&slot)[MTR], const AOp& A, const AOp& N, int s) {
+#if AVC_FZ_ABLATE & 4
+    const bool own = true;   // debug: no cross-GEMM prefetch (N's steps loaded as A's last)
+#else
+    const bool own = s < A.ns;
+#endif
+    const f32x4* base = own ? a_step(A, s) : a_step(N, s - A.ns > 0 ? s - A.ns : 0);
+    const int amt = own ? A.amt : N.amt;
+    const int mt = own ? A.mt : N.mt;
+#pragma unroll
+    for (int i = 0; i < MTR; ++i)
+        slot[i] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
+            (const __attribute__((address_space(1))) f32x4*)(base + (size_t)(i < mt ? i : mt - 1) * amt));
+#if AVC_FZ_ABLATE & 1
+#pragma unroll
+    for (int i = 0; i < MTR; ++i) slot[i] = f32x4{0.001f * s, 0.f, 0.f, 0.f};
+#endif
+}
+template <int MTR>
+__device__ __forceinline__ void ring_fill(ARing<MTR>& R, const AOp& A) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ring_load<MTR>(R.a[u], A, A, u);
+}
+
+// acc[MT][NF] += A x B; the ring holds A's steps 0..3 on entry and N's steps 0..3 on exit.
+//   B  : LDS base of the operand image; rb[f] = row of tap 0 for this lane's column
+//   DJ : +1 forward (row = rb + j), -1 adjoint (row = rb - j)
+// B fragments are read one step ahead into two alternating register sets.  The loop
+// body has no early exits and issues every load unconditionally (steps past the end
+// are clamped), so accumulators keep their registers across the back edge and the
+// waitcnt pass sees a fixed number of loads in flight.
 // NFC > 0: the live fragment count is the compile-time NFC (straight-line K loop);
 // NFC == 0: up to NF fragments, the first `nf` live (runtime guards; generic shapes).
-template <int PREC, int MT, int NF, int NFC, int CINB, int DJ>
-__device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, const f32x4* __restrict__ Ap, int amt,
-                                             const char* B, const int (&rb)[NF], int ns, int lg, int msk, int spt,
-                                             int soff) {
+template <int PREC, int MT, int MTR, int NF, int NFC, int CINB, int DJ>
+__device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing<MTR>& R, const AOp& A,
+                                             const AOp& N, const char* B, const int (&rb)[NF]) {
+    static_assert(MT <= MTR, "ring narrower than the GEMM");
     constexpr int NL = NFC ? NFC : NF;                 // fragments the loops run over
     auto live = [&](int f) __attribute__((always_inline)) { return NFC ? f < NFC : f < nf; };
     using E = typename Fz<PREC>::E;
@@ -125,62 +187,96 @@ __device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, const
     constexpr int VE = 16 / (int)sizeof(E);
     constexpr int KS = 4 * VE;
     const int kq = (threadIdx.x & 63) >> 4;
+    const int ns = A.ns;
     int rbo[NL];
 #pragma unroll
     for (int f = 0; f < NL; ++f) rbo[f] = rb[f] * RS;
-    auto ps_of = [&](int s) __attribute__((always_inline)) { return (s >> lg) * spt + soff + (s & msk); };
-    auto load_a = [&](f32x4 (&a)[MT], int s) __attribute__((always_inline)) {
-        if (s < ns) {
-            const int ps = ps_of(s);
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-                a[i] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
-                    (const __attribute__((address_space(1))) f32x4*)(Ap + (size_t)i * amt + (size_t)ps * 64));
-        }
-    };
     auto read_b = [&](f32x4 (&b)[NL], int s) __attribute__((always_inline)) {
-        if (s < ns) {
-            const int kl = KS * ps_of(s) + VE * kq;
-            const int j = kl / CINB;
-            const int ci = kl - j * CINB;
-            const char* Bs = B + ci * (int)sizeof(E) + DJ * j * RS;
+        s = s < ns ? s : ns - 1;
+        const int kl = KS * ((s >> A.lg) * A.spt + A.soff + (s & A.msk)) + VE * kq;
+        const int j = kl / CINB;
+        const int ci = kl - j * CINB;
+        const char* Bs = B + ci * (int)sizeof(E) + DJ * j * RS;
 #pragma unroll
-            for (int f = 0; f < NL; ++f)
-                if (live(f)) b[f] = lds16(Bs + rbo[f]);
-        }
+        for (int f = 0; f < NL; ++f)
+            if (live(f)) b[f] = lds16(Bs + rbo[f]);
     };
-    auto mma_all = [&](const f32x4 (&a)[MT], const f32x4 (&b)[NL]) __attribute__((always_inline)) {
+    auto mma_all = [&](const f32x4 (&a)[MTR], const f32x4 (&b)[NL]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int f = 0; f < NL; ++f)
                 if (live(f)) mma<PREC>(acc[i][f], a[i], b[f]);
     };
-    f32x4 a0[MT], a1[MT], a2[MT], a3[MT];
     f32x4 bA[NL], bB[NL];
-    load_a(a0, 0);
-    load_a(a1, 1);
-    load_a(a2, 2);
-    load_a(a3, 3);
     read_b(bA, 0);
+    const int nfull = ns & ~3;
 #pragma unroll 1
-    for (int s = 0; s < ns; s += 4) {
+    for (int s = 0; s < nfull; s += 4) {
         read_b(bB, s + 1);
-        mma_all(a0, bA);
-        load_a(a0, s + 4);
-        if (s + 1 >= ns) break;
+        mma_all(R.a[0], bA);
+        ring_load<MTR>(R.a[0], A, N, s + 4);
         read_b(bA, s + 2);
-        mma_all(a1, bB);
-        load_a(a1, s + 5);
-        if (s + 2 >= ns) break;
+        mma_all(R.a[1], bB);
+        ring_load<MTR>(R.a[1], A, N, s + 5);
         read_b(bB, s + 3);
-        mma_all(a2, bA);
-        load_a(a2, s + 6);
-        if (s + 3 >= ns) break;
+        mma_all(R.a[2], bA);
+        ring_load<MTR>(R.a[2], A, N, s + 6);
         read_b(bA, s + 4);
-        mma_all(a3, bB);
-        load_a(a3, s + 7);
+        mma_all(R.a[3], bB);
+        ring_load<MTR>(R.a[3], A, N, s + 7);
     }
+    // remainder (0..3 steps): slots hold steps nfull..nfull+3 (slot u = step nfull+u),
+    // bA holds step nfull.  Afterwards rotate so that slot u = N's step u again.
+    const int rem = ns - nfull;
+#if AVC_FZ_ABLATE & 4
+    // debug: no cross-GEMM prefetch -- finish this GEMM's own steps, then load N afresh
+    if (rem >= 1) mma_all(R.a[0], bA);
+    if (rem >= 2) {
+        read_b(bB, nfull + 1);
+        mma_all(R.a[1], bB);
+    }
+    if (rem >= 3) {
+        read_b(bA, nfull + 2);
+        mma_all(R.a[2], bA);
+    }
+    ring_fill(R, N);
+    return;
+#endif
+    if (rem == 0) return;
+    mma_all(R.a[0], bA);
+    ring_load<MTR>(R.a[0], A, N, nfull + 4);
+    if (rem >= 2) {
+        read_b(bB, nfull + 1);
+        mma_all(R.a[1], bB);
+        ring_load<MTR>(R.a[1], A, N, nfull + 5);
+    }
+    if (rem >= 3) {
+        read_b(bA, nfull + 2);
+        mma_all(R.a[2], bA);
+        ring_load<MTR>(R.a[2], A, N, nfull + 6);
+    }
+    // a GEMM shorter than the ring (ns < 4) entered with slots u >= ns holding clamped
+    // copies of its own last step (its predecessor could not know this GEMM's successor):
+    // those slots get N's steps u - rem now
+    if (nfull == 0)
+        for (int u = rem; u < 4; ++u) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                if (v == u) ring_load<MTR>(R.a[v], N, N, u - rem);
+        }
+    // slot u now holds step nfull + u + 4*(u < rem) of the A|N stream, i.e. N's step
+    // (u - rem) mod 4: rotate left by rem
+    f32x4 t[4][MTR];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < MTR; ++i) t[u][i] = R.a[u][i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < MTR; ++i)
+            R.a[u][i] = rem == 1 ? t[(u + 1) & 3][i] : (rem == 2 ? t[(u + 2) & 3][i] : t[(u + 3) & 3][i]);
 }
 
 template <int V>
@@ -188,18 +284,16 @@ using IC = std::integral_constant<int, V>;
 
 // fz_gemm: the fragment count is either a compile-time IC<N> (specialised shapes) or a
 // runtime int (generic shapes)
-template <int PREC, int MT, int NF, int CINB, int DJ, int N>
-__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], IC<N>, const f32x4* __restrict__ Ap, int amt,
-                                        const char* B, const int (&rb)[NF], int ns, int lg = 30, int msk = -1,
-                                        int spt = 0, int soff = 0) {
-    static_assert(N >= 1 && N <= NF, "fragment count");
-    fz_gemm_impl<PREC, MT, NF, N, CINB, DJ>(acc, N, Ap, amt, B, rb, ns, lg, msk, spt, soff);
+template <int PREC, int MT, int NF, int CINB, int DJ, int MTR, int NFC>
+__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], IC<NFC>, ARing<MTR>& R, const AOp& A, const AOp& N,
+                                        const char* B, const int (&rb)[NF]) {
+    static_assert(NFC >= 1 && NFC <= NF, "fragment count");
+    fz_gemm_impl<PREC, MT, MTR, NF, NFC, CINB, DJ>(acc, NFC, R, A, N, B, rb);
 }
-template <int PREC, int MT, int NF, int CINB, int DJ>
-__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], int nf, const f32x4* __restrict__ Ap, int amt,
-                                        const char* B, const int (&rb)[NF], int ns, int lg = 30, int msk = -1,
-                                        int spt = 0, int soff = 0) {
-    fz_gemm_impl<PREC, MT, NF, 0, CINB, DJ>(acc, nf, Ap, amt, B, rb, ns, lg, msk, spt, soff);
+template <int PREC, int MT, int NF, int CINB, int DJ, int MTR>
+__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], int nf, ARing<MTR>& R, const AOp& A, const AOp& N,
+                                        const char* B, const int (&rb)[NF]) {
+    fz_gemm_impl<PREC, MT, MTR, NF, 0, CINB, DJ>(acc, nf, R, A, N, B, rb);
 }
 
 template <int I, int N, class F>
@@ -259,6 +353,7 @@ __device__ __forceinline__ void fold_edges(f32x4 (&acc)[MT][NF], int Tin, int E,
 struct MaskAcc {
     u64 lo = 0, hi = 0;
     __device__ __forceinline__ void put(int widx, u64 word) {
+        if (AVC_FZ_ABLATE & 2) return;
         const int lane = threadIdx.x & 63;
         if (widx < 64) {
             if (lane == widx) lo = word;
@@ -288,10 +383,14 @@ __device__ __forceinline__ void put_reflect(char* img, int t, int T, int P, int 
 }
 
 // ---------------------------------------------------------------------------------
-// shapes: STD = the AdaIN-VC speaker encoder at its config.yaml defaults (bank 1..8,
-// kernel 5, six blocks with subsample [1,2,1,2,1,2]) at T = 128 -- every layer's frame
-// and fragment count is a compile-time constant.  STD = 0: the same code on runtime
-// shapes (any T <= 128, any eligible config).
+// shapes (kernel template parameter SH):
+//   SH = 0        : the AdaIN-VC speaker encoder at its config.yaml defaults (bank 1..8,
+//                   kernel 5, six blocks with subsample [1,2,1,2,1,2]) at T = 128 -- every
+//                   layer's frame and fragment count is a compile-time constant;
+//   SH = 1,2,4,8  : any eligible config and T <= 16*SH; every layer runs SH fragments
+//                   (SH + 1 for dgrad outputs, which carry the pad-position columns).
+// Fragment counts are never runtime values: MFMA code under runtime per-fragment
+// guards produced wrong results on gfx950 for one-fragment layers.
 // ---------------------------------------------------------------------------------
 struct StdSE {
     static constexpr int T = 128, NB = 8, KSZ = 5, NBLK = 6;
@@ -304,19 +403,14 @@ struct StdSE {
     static constexpr int nf(int frames) { return (frames + 15) / 16; }
 };
 
-template <int STD, int V>
-__device__ __forceinline__ auto shape_nf(int rt) {
-    if constexpr (STD != 0)
-        return IC<V>{};
-    else
-        return rt;
-}
 
 // ---------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------
-template <int PREC, int STD>
+template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
+    constexpr int STD = SH == 0 ? 1 : 0;
+    constexpr int G = SH == 0 ? 8 : SH;         // fragments per (non-dgrad) layer
     using E = typename Fz<PREC>::E;
     constexpr int RS = Fz<PREC>::RS;
     constexpr int ESZ = (int)sizeof(E);
@@ -326,6 +420,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     const int b = blockIdx.x;
     const int T = STD ? StdSE::T : A.T;
     const int nb = STD ? StdSE::NB : A.nb;
+    const int nblk = STD ? StdSE::NBLK : A.nblk;
     const int ks = STD ? StdSE::KSZ : A.ks;
     const int P = ks / 2;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -343,7 +438,6 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     u64* mbase = A.masks + (size_t)b * A.mask_words;
     const bool wm = A.write_masks != 0;
     const int ch0 = 32 * w + 4 * kq;                    // + 16*i + r
-    const int lane_off = lane;                          // f32x4 units inside a packed step
     constexpr int WPL = FZ_MASK_WORDS_PER_LAYER / 4;    // mask words per (layer, wave)
 
     // ---- x -> XB (transposed, reflect rows)
@@ -359,7 +453,22 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     }
     __syncthreads();
 
-    const auto nf0 = shape_nf<STD, StdSE::nf(StdSE::T)>((T + 15) >> 4);
+    const auto nf0 = IC<G>{};
+    const int ns_c = ks * FZ_C / KS;
+    // the A operands of the pass, in launch order (each GEMM prefetches the next one's)
+    auto op_bank = [&](int kb) __attribute__((always_inline)) {
+        const int ns = (FZ_CIN * (kb + 1) + KS - 1) / KS;
+        return aop(A.w.bank[kb], 2 * w, 2, ns, ns);
+    };
+    auto op_inb = [&](int kb) __attribute__((always_inline)) { return aop(A.w.in_b[kb], 2 * w, 2, FZ_C / KS, FZ_C / KS); };
+    auto op_inx = [&]() __attribute__((always_inline)) {
+        const int ns = (FZ_CIN + KS - 1) / KS;
+        return aop(A.w.in_x, 2 * w, 2, ns, ns);
+    };
+    auto op_c1 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2[l], 2 * w, 2, ns_c, ns_c); };
+    ARing<2> ring;
+    ring_fill(ring, op_bank(0));
     int rb[NF];
     f32x4 acc_h[2][NF];
     zero_acc(acc_h);
@@ -371,9 +480,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         zero_acc(acc);
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, T - 1) + 4 - pl;
-        const int ns = (FZ_CIN * k + KS - 1) / KS;
-        const f32x4* Ap = reinterpret_cast<const f32x4*>(A.w.bank[kb]) + (size_t)(2 * w) * ns * 64 + lane_off;
-        fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc, nf0, Ap, ns * 64, XB, rb, ns);
+        fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc, nf0, ring, op_bank(kb), op_inb(kb), XB, rb);
         char* BK = (kb & 1) ? BK1 : BK0;
         const float* bias = A.w.b_bank[kb];
         mk = MaskAcc();
@@ -398,17 +505,13 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         // in_conv over this bank block (K = 128 channels of the block)
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, T - 1);
-        const int ns2 = FZ_C / KS;
-        const f32x4* Ai = reinterpret_cast<const f32x4*>(A.w.in_b[kb]) + (size_t)(2 * w) * ns2 * 64 + lane_off;
-        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc_h, nf0, Ai, ns2 * 64, BK, rb, ns2);
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc_h, nf0, ring, op_inb(kb), kb + 1 < nb ? op_bank(kb + 1) : op_inx(), BK, rb);
         if (!DBUF) __syncthreads();
     }
     {   // in_conv, x block (K = 80)
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, T - 1) + 4;
-        const int ns = (FZ_CIN + KS - 1) / KS;
-        const f32x4* Ai = reinterpret_cast<const f32x4*>(A.w.in_x) + (size_t)(2 * w) * ns * 64 + lane_off;
-        fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc_h, nf0, Ai, ns * 64, XB, rb, ns);
+        fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc_h, nf0, ring, op_inx(), op_c1(0), XB, rb);
     }
     __syncthreads();   // XB / BK are dead: HB and YB alias them
 
@@ -436,7 +539,6 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     }
     __syncthreads();
 
-    const int ns_c = ks * FZ_C / KS;
     // one conv block (models.py:285-305); nfi / nfo: fragments of its input / output frames
     auto block = [&](auto nfi, auto nfo, int l, int Ti, int To, int s) __attribute__((always_inline)) {
         f32x4 acc[2][NF];
@@ -444,10 +546,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         zero_acc(acc);
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, Ti - 1);
-        {
-            const f32x4* Ap = reinterpret_cast<const f32x4*>(A.w.c1[l]) + (size_t)(2 * w) * ns_c * 64 + lane_off;
-            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, Ap, ns_c * 64, HB, rb, ns_c);
-        }
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c1(l), op_c2(l), HB, rb);
         mk = MaskAcc();
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -471,10 +570,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         zero_acc(acc);
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, To - 1) * s;
-        {
-            const f32x4* Ap = reinterpret_cast<const f32x4*>(A.w.c2[l]) + (size_t)(2 * w) * ns_c * 64 + lane_off;
-            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfo, Ap, ns_c * 64, YB, rb, ns_c);
-        }
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfo, ring, op_c2(l), l + 1 < nblk ? op_c1(l + 1) : op_c2(l), YB, rb);
         if (s == 2) {
             // pooled[t'] = (h[2t'] + h[2t'+1]) / cnt : sources in frags 2f', 2f'+1; increasing f'
             // order keeps the in-place update safe (frag f' is read before it is written)
@@ -532,7 +628,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         TN = StdSE::Tl(StdSE::NBLK);
     } else {
         for (int l = 0; l < A.nblk; ++l)
-            block((A.Tl[l] + 15) >> 4, (A.Tl[l + 1] + 15) >> 4, l, A.Tl[l], A.Tl[l + 1], A.sub[l]);
+            block(IC<G>{}, IC<G>{}, l, A.Tl[l], A.Tl[l + 1], A.sub[l]);
         TN = A.Tl[A.nblk];
     }
 
@@ -559,8 +655,10 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 // ---------------------------------------------------------------------------------
 // backward + Adam
 // ---------------------------------------------------------------------------------
-template <int PREC, int STD>
+template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
+    constexpr int STD = SH == 0 ? 1 : 0;
+    constexpr int G = SH == 0 ? 8 : SH;
     using E = typename Fz<PREC>::E;
     constexpr int RS = Fz<PREC>::RS;
     constexpr int ESZ = (int)sizeof(E);
@@ -580,7 +678,6 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const int c = lane & 15, kq = lane >> 4;
     const int act = A.act;
     const int ch0 = 32 * w + 4 * kq;
-    const int lane_off = lane;
     const u64* mbase = A.masks + (size_t)b * A.mask_words;
     auto mword = [&](int layer, int widx) __attribute__((always_inline)) -> u64 {
         return mbase[(size_t)(layer * 4 + w) * WPL + widx];
@@ -608,6 +705,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     __syncthreads();
 
     const int ns_c = ks * FZ_C / KS;
+    const int nblk = STD ? StdSE::NBLK : A.nblk;
+    auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2T[l], 2 * w, 2, ns_c, ns_c); };
+    ARing<2> ring;
+    ring_fill(ring, op_c2T(nblk - 1));
     int rb[NF];
     // backward of one conv block; nfo: fragments of its output frames, nfc: of the
     // dgrad columns (Ti interior frames + 2P pad positions)
@@ -642,10 +744,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         }
         f32x4 acc[2][NF];
         zero_acc(acc);
-        {
-            const f32x4* Ap = reinterpret_cast<const f32x4*>(A.w.c2T[l]) + (size_t)(2 * w) * ns_c * 64 + lane_off;
-            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, Ap, ns_c * 64, GB, rb, ns_c);
-        }
+        fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l), op_c1T(l), GB, rb);
         fold_edges(acc, Ti, P, FSCR);
         {   // * act'(y1_l) -> GB2 (stride 1)
             const int L1 = nb + 1 + 2 * l;
@@ -665,10 +764,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         __syncthreads();
         // conv1^T (+ fold) + avg_pool^T of g(h_{l+1}) -> g(h_l)
         zero_acc(acc);
-        {
-            const f32x4* Ap = reinterpret_cast<const f32x4*>(A.w.c1T[l]) + (size_t)(2 * w) * ns_c * 64 + lane_off;
-            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, Ap, ns_c * 64, GB2, rb, ns_c);
-        }
+        fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c1T(l), l > 0 ? op_c2T(l - 1) : op_c1T(l), GB2, rb);
         fold_edges(acc, Ti, P, FSCR);
         if (s == 2) {
             // g_h[t] += g_{l+1}[t/2] / cnt(t/2) (torch avg_pool backward: grad / divide_factor);
@@ -710,12 +806,12 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         });
     } else {
         for (int l = A.nblk - 1; l >= 0; --l)
-            block((A.Tl[l + 1] + 15) >> 4, (A.Tl[l] + 2 * P + 15) >> 4, l, A.Tl[l], A.Tl[l + 1], A.sub[l]);
+            block(IC<G>{}, IC<G + 1>{}, l, A.Tl[l], A.Tl[l + 1], A.sub[l]);
     }
 
     // g_pre0 = g(h0) * act'(h0) -> GP (= GB image, rows ZP + t; pad rows are zero)
     char* GP = GB;
-    const auto nf0 = shape_nf<STD, StdSE::nf(StdSE::T)>((T + 15) >> 4);
+    const auto nf0 = IC<G>{};
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -740,20 +836,26 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
             *reinterpret_cast<f32x4*>(GBK + row * RS + 32 * w * ESZ + part * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
-    const auto nfx = shape_nf<STD, StdSE::nf(StdSE::T + 2 * EB)>((T + 2 * EB + 15) >> 4);
+    const auto nfx = IC<STD ? StdSE::nf(StdSE::T + 2 * EB) : G + 1>{};
     f32x4 accx[5][NF];
     zero_acc(accx);
     constexpr int SPW = 32 / KS;                // K steps of one wave's 32-channel quarter
     constexpr int SPT = FZ_C / KS;              // K steps per tap
     constexpr int LG = SPW == 1 ? 0 : 1;
+    auto op_inTb = [&](int kb) __attribute__((always_inline)) { return aop(A.w.inT_b[kb], 2 * w, 2, SPT, SPT); };
+    auto op_bankT = [&](int kb) __attribute__((always_inline)) {
+        return aop(A.w.bankT[kb], 0, 5, (kb + 1) * SPT, (kb + 1) * SPW, LG, SPW - 1, SPT, w * SPW);
+    };
+    ARing<5> ring5;
     {   // x passthrough of the cat: W_in[:, x block]^T g_pre0 (interior columns only)
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
             const int n = 16 * f + c;
             rb[f] = n < T ? ZP + n : 0;
         }
-        const f32x4* Ap = reinterpret_cast<const f32x4*>(A.w.inT_x) + lane_off;
-        fz_gemm<PREC, 5, NF, FZ_C, 1>(accx, nfx, Ap, SPT * 64, GP, rb, SPW, 30, -1, 0, w * SPW);
+        const AOp opx = aop(A.w.inT_x, 0, 5, SPT, SPW, 30, -1, 0, w * SPW);
+        ring_fill(ring5, opx);
+        fz_gemm<PREC, 5, NF, FZ_C, 1>(accx, nfx, ring5, opx, op_inTb(0), GP, rb);
     }
     for (int kb = 0; kb < nb; ++kb) {
         const int k = kb + 1, pl = k / 2;
@@ -763,10 +865,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         int rt[8];
 #pragma unroll
         for (int f = 0; f < 8; ++f) rt[f] = ZP + min(16 * f + c, T - 1);
-        {
-            const f32x4* Ap = reinterpret_cast<const f32x4*>(A.w.inT_b[kb]) + (size_t)(2 * w) * SPT * 64 + lane_off;
-            fz_gemm<PREC, 2, 8, FZ_C, 1>(acc, nf0, Ap, SPT * 64, GP, rt, SPT);
-        }
+        fz_gemm<PREC, 2, 8, FZ_C, 1>(acc, nf0, ring5, op_inTb(kb), op_bankT(kb), GP, rt);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -785,8 +884,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
             const int n = 16 * f + c;
             rb[f] = ZPB + (n < T + 2 * EB ? vpos(n, T, EB) : 0) + pl;
         }
-        const f32x4* Ap = reinterpret_cast<const f32x4*>(A.w.bankT[kb]) + lane_off;
-        fz_gemm<PREC, 5, NF, FZ_C, -1>(accx, nfx, Ap, k * SPT * 64, GBK, rb, k * SPW, LG, SPW - 1, SPT, w * SPW);
+        fz_gemm<PREC, 5, NF, FZ_C, -1>(accx, nfx, ring5, op_bankT(kb), kb + 1 < nb ? op_inTb(kb + 1) : op_bankT(kb), GBK, rb);
         __syncthreads();
     }
     fold_edges(accx, T, EB, FSCR);
@@ -844,8 +942,14 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     template __global__ void se_bwd_fused<P, S>(FusedArgs);
 AVC_FZ_INST(PREC_F32, 0)
 AVC_FZ_INST(PREC_F32, 1)
+AVC_FZ_INST(PREC_F32, 2)
+AVC_FZ_INST(PREC_F32, 4)
+AVC_FZ_INST(PREC_F32, 8)
 AVC_FZ_INST(PREC_BF16, 0)
 AVC_FZ_INST(PREC_BF16, 1)
+AVC_FZ_INST(PREC_BF16, 2)
+AVC_FZ_INST(PREC_BF16, 4)
+AVC_FZ_INST(PREC_BF16, 8)
 #undef AVC_FZ_INST
 
 }  // namespace avc

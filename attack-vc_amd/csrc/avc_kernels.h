@@ -103,6 +103,8 @@ struct HeadArgs {
     int32_t B, C, TN, D, n_dense, act, mode;
     const float* pooled_in;   // fused path: [B][C] time-mean of h_N (replaces the hN pooling)
     float* g_pooled;          // fused path: [B][C] d loss / d pooled (replaces the g_hN expansion)
+    const float* Wr;          // se_head_v: row-major dense [2nd][C][C], output [D][C]
+    const float* WrT;         // se_head_v: their transposes [2nd][C][C], output^T [C][D]
 };
 
 // ---------------------------------------------------------------------------------

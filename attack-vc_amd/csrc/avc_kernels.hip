@@ -280,6 +280,284 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// se_head_v: the same chain for the fused engine (time-mean in, its gradient out), on
+// the VALU with HV = 2 utterances per workgroup (128 CUs share a B = 256 batch);
+// c_h = c_out = 128 (the fused engine's shape).
+// The chain is bound by streaming its 26 weight matrices (1.7 MB fp32) through each
+// workgroup and by LDS reads of the input vector, not by arithmetic.  Thread
+// (row m = tid/4, slice q = tid%4) owns the K/4 weights W[m][8i + 2q + e] (i < K/8,
+// e < 2) -- stored contiguously by the host packer (Wr/WrT are row-permuted) -- so the
+// four slices of a row read adjacent 16-byte chunks of the [k][utterance] input
+// (conflict-free, broadcast over the 16 rows of a wave).  Its 2 partial dot products
+// are summed over q with two xor-shuffles.  Weights are fetched four steps ahead (each
+// step otherwise waits a full MALL round trip).
+// Step i (0 <= i < NL, nf = 2nd + 1 forward steps):
+//   i <  2nd : Y_i = act(W_i X + b_i), X = E (i even) / Y_{i-1} (i odd); E += Y_i (i odd)
+//   i == 2nd : EMB = W_out E + b_out;  loss and GA = d loss / d EMB
+//   i == nf  : GB = W_out^T GA;                GM = GB * act'(Y_{2nd-1})
+//   j = i-nf-1 even (l = nd-1-j/2): GA = (W_{2l+1}^T GM) * act'(Y_{2l})
+//   j odd            : GB += W_{2l}^T GA;      GM = GB * act'(Y_{2l-1})  (l > 0)
+// ---------------------------------------------------------------------------------
+constexpr int HV = 2;
+#ifndef AVC_HEAD_ABLATE
+#define AVC_HEAD_ABLATE 0
+#endif
+
+struct HeadVW {
+    f32x4 w[8];   // K/4 <= 32 weights of one row slice
+};
+
+__global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
+    // no contraction: an utterance's arithmetic must not depend on its lane in the pair
+#pragma clang fp contract(off)
+    extern __shared__ float smem[];
+    // every field the chain uses, hoisted out of the kernel-argument struct (lambdas that
+    // capture the by-value argument by reference would spill it to scratch)
+    const int C = A.C, D = A.D, nd = A.n_dense, act = A.act, Bn = A.B, mode = A.mode;
+    const float* __restrict__ Wr = A.Wr;
+    const float* __restrict__ WrT = A.WrT;
+    float* __restrict__ losses = A.losses;
+    const int loss_len = A.loss_len;
+    const int CM = C > D ? C : D;
+    f32x2* E = reinterpret_cast<f32x2*>(smem);     // [CM] x 2 utterances
+    f32x2* Ys = E + CM;                             // [2nd][CM]
+    f32x2* EMB = Ys + 2 * nd * CM;
+    f32x2* GA = EMB + CM;
+    f32x2* GB = GA + CM;
+    f32x2* GM = GB + CM;
+    // biases and loss targets staged in LDS before the weight prefetch starts: vmcnt
+    // retires in order, so a late per-row global load would drain the whole prefetch
+    float* Bs = reinterpret_cast<float*>(GM + CM);  // [2nd*C + D]
+    f32x2* TG = reinterpret_cast<f32x2*>(Bs + 2 * nd * C + D);   // [D]: tgt of both utterances
+    f32x2* OG = TG + D;                                           // [D]: org
+    float* LS = reinterpret_cast<float*>(OG + D);                 // [HV] per-utterance loss
+
+    const int tid = threadIdx.x, m = tid >> 2, q = tid & 3;
+    const int u0 = blockIdx.x * HV;
+    for (int idx = tid; idx < 2 * nd * C + D; idx += blockDim.x) Bs[idx] = A.bias[idx];
+    if (mode != 0)
+        for (int idx = tid; idx < D * HV; idx += blockDim.x) {
+            const int d = idx / HV, u = idx - d * HV;
+            const int b = u0 + u;
+            reinterpret_cast<float*>(TG)[idx] = b < Bn ? A.tgt[(size_t)b * D + d] : 0.f;
+            reinterpret_cast<float*>(OG)[idx] = b < Bn ? A.org[(size_t)b * D + d] : 0.f;
+        }
+    for (int idx = tid; idx < C * HV; idx += blockDim.x) {
+        const int c = idx / HV, u = idx - c * HV;
+        const int b = u0 + u;
+        reinterpret_cast<float*>(E)[idx] = b < Bn ? A.pooled_in[(size_t)b * C + c] : 0.f;
+    }
+    const size_t CC = (size_t)C * C;
+    const int nf = 2 * nd + 1;
+    const int NL = mode == 0 ? nf : 2 * nf;
+
+    // weights of chain step i (see the table above); every step is 128 x 128
+    auto step_w = [=](int i) __attribute__((always_inline)) -> const float* {
+        if (i < 2 * nd + 1) return Wr + (size_t)i * CC;              // dense layers, then output
+        if (i == nf) return WrT + (size_t)(2 * nd) * CC;              // output^T
+        const int j = i - nf - 1;
+        const int l = nd - 1 - j / 2;
+        return WrT + (size_t)(j % 2 == 0 ? 2 * l + 1 : 2 * l) * CC;
+    };
+    // C == D == 128 (fused engine): every step is a 128 x 128 matrix, K/4 = 32 weights
+    // per thread -- eight unconditional 16-byte loads, no branches for the waitcnt
+    // pass to be conservative about
+    auto load_w = [&](HeadVW& hw, int i) __attribute__((always_inline)) {
+        const float* row = step_w(i) + (size_t)m * 128 + q * 32;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+#if AVC_HEAD_ABLATE & 1
+            hw.w[e] = f32x4{0.01f * i, 0.02f, 0.03f, 0.04f * e};
+#else
+            hw.w[e] = gload<f32x4>(row + 4 * e);
+#endif
+        }
+    };
+    // out[m] (2 utterances) = sum_k W[m][k] X[k], summed over the 4 slices
+    auto dot = [&](const HeadVW& hw, int K, const f32x2* X) __attribute__((always_inline)) -> f32x2 {
+        (void)K;
+        f32x2 acc = {0.f, 0.f}, acc2 = {0.f, 0.f};   // even / odd k of the pair
+        const f32x4* X4 = reinterpret_cast<const f32x4*>(X);   // {X[k][0], X[k][1], X[k+1][0], X[k+1][1]}
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {   // i = 2e + h  ->  k = 8i + 2q
+#if AVC_HEAD_ABLATE & 2
+                const f32x4 x = f32x4{acc[0], acc[1], 0.5f, 0.25f};
+#else
+                const f32x4 x = X4[4 * (2 * e + h) + q];
+#endif
+                // explicit fma chain: both utterance lanes round identically (shard invariance)
+                acc[0] = fmaf(hw.w[e][2 * h], x[0], acc[0]);
+                acc[1] = fmaf(hw.w[e][2 * h], x[1], acc[1]);
+                acc2[0] = fmaf(hw.w[e][2 * h + 1], x[2], acc2[0]);
+                acc2[1] = fmaf(hw.w[e][2 * h + 1], x[3], acc2[1]);
+            }
+        }
+        acc[0] = acc[0] + acc2[0];
+        acc[1] = acc[1] + acc2[1];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            acc[r] += __shfl_xor(acc[r], 1);
+            acc[r] += __shfl_xor(acc[r], 2);
+        }
+        return acc;
+    };
+
+    // L2 warm-up: the conv kernels between two head launches evict these weights, and
+    // the chain steps would otherwise each pay a MALL round trip.  Workgroups with the
+    // same blockIdx % 8 are dispatched to the same XCD (MI355X_MICROARCH.md, dispatch):
+    // together they stream the whole 1.7 MB set once into their XCD's L2 (a
+    // performance hint only -- any placement stays correct).
+    {
+        const int grp = (int)(blockIdx.x >> 3), ngrp = (int)((gridDim.x + 7) >> 3);
+        const size_t n4 = (size_t)(2 * nd + 1) * CC / 4;        // f32x4 per matrix set
+        const f32x4* W4[2] = {reinterpret_cast<const f32x4*>(Wr), reinterpret_cast<const f32x4*>(WrT)};
+        float sink = 0.f;
+        for (int t = 0; t < 2; ++t)
+            for (size_t i = (size_t)grp * blockDim.x + tid; i < n4; i += (size_t)ngrp * blockDim.x) {
+                const f32x4 v = gload<f32x4>(reinterpret_cast<const float*>(W4[t] + i));
+                sink += v[0];
+            }
+        if (sink == 1.2345e-31f && tid == 1023) A.g_pooled[0] = sink;   // keeps the loads; never true
+    }
+    const float gscale = A.scal[1];
+    const int step_no = mode == 0 ? 0 : *A.step;
+    __syncthreads();
+    HeadVW w0, w1, w2, w3;
+    load_w(w0, 0);
+    load_w(w1, min(1, NL - 1));
+    load_w(w2, min(2, NL - 1));
+    load_w(w3, min(3, NL - 1));
+
+    auto run_step = [&](int i, const HeadVW& hw) __attribute__((always_inline)) {
+        constexpr int K = 128;
+        const bool own = q == 0;
+        if (i < 2 * nd) {
+            // (E is written only by odd steps, which read Y_{i-1}: no hazard inside a step)
+            const f32x2 o = dot(hw, K, (i % 2 == 0) ? E : Ys + (i - 1) * CM);
+            if (own) {
+                const float bi = Bs[i * C + m];
+                f32x2 y;
+#pragma unroll
+                for (int r = 0; r < 2; ++r) y[r] = act_f(o[r] + bi, act);
+                Ys[i * CM + m] = y;
+                if (i % 2 == 1) E[m] = y + E[m];
+            }
+        } else if (i == 2 * nd) {
+            const f32x2 o = dot(hw, K, E);
+            if (own) {
+                const f32x2 e = o + Bs[2 * nd * C + m];
+                EMB[m] = e;
+                if (mode != 0) {
+                    // loss = MSE(emb, tgt) - 0.1 MSE(emb, org) (attack_utils.py:81-82)
+                    f32x2 g, q1, q2;
+#pragma unroll
+                    for (int u = 0; u < HV; ++u) {
+                        const int b = u0 + u;
+                        float gg = 0.f, a1 = 0.f, a2 = 0.f;
+                        if (b < Bn) {
+                            const float d1 = e[u] - TG[m][u];
+                            const float d2 = e[u] - OG[m][u];
+                            gg = gscale * d1 + gscale * d2 * -0.1f;
+                            a1 = d1 * d1;
+                            a2 = d2 * d2;
+                        }
+                        g[u] = gg;
+                        q1[u] = a1;
+                        q2[u] = a2;
+                    }
+                    GA[m] = g;
+                    GB[m] = q1;   // scratch for the loss sums (GB is rewritten by step nf)
+                    GM[m] = q2;
+                }
+            }
+            __syncthreads();
+            if (mode != 0 && tid < 64 * HV) {
+                // per-utterance loss: wave u sums over d in a fixed order (stored at the end)
+                const int u = tid >> 6, lane = tid & 63;
+                float s1 = 0.f, s2 = 0.f;
+                for (int d = lane; d < D; d += 64) {
+                    s1 += GB[d][u];
+                    s2 += GM[d][u];
+                }
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    s1 += __shfl_xor(s1, o);
+                    s2 += __shfl_xor(s2, o);
+                }
+                if (lane == 0) LS[u] = s1 / (float)D - 0.1f * (s2 / (float)D);
+            }
+        } else if (i == nf) {
+            const f32x2 o = dot(hw, K, GA);
+            if (own) {   // (the loss sums of step 2nd read GB/GM before that step's last barrier)
+                GB[m] = o;
+                const f32x2 y = Ys[(2 * nd - 1) * CM + m];
+                GM[m] = f32x2{o[0] * act_d(y[0], act), o[1] * act_d(y[1], act)};
+            }
+        } else {
+            const int j = i - nf - 1;
+            const int l = nd - 1 - j / 2;
+            if (j % 2 == 0) {
+                const f32x2 o = dot(hw, K, GM);
+                if (own) {
+                    const f32x2 y = Ys[(2 * l) * CM + m];
+                    GA[m] = f32x2{o[0] * act_d(y[0], act), o[1] * act_d(y[1], act)};
+                }
+            } else {
+                const f32x2 o = dot(hw, K, GA);
+                if (own) {
+                    const f32x2 gb = GB[m] + o;
+                    GB[m] = gb;
+                    if (l > 0) {
+                        const f32x2 y = Ys[(2 * l - 1) * CM + m];
+                        GM[m] = f32x2{gb[0] * act_d(y[0], act), gb[1] * act_d(y[1], act)};
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    };
+
+    // static 4-step register ring: slot u holds step i+u and is refilled with step
+    // i+4+u right after its step.  Refills are unconditional (clamped to the last step)
+    // and the loop has no early exits: on a conditional path the waitcnt pass would
+    // have to assume the newest loads are the ones awaited and drain the whole ring.
+    const int nfull = NL & ~3;
+    for (int i = 0; i < nfull; i += 4) {
+        run_step(i, w0);
+        load_w(w0, min(i + 4, NL - 1));
+        run_step(i + 1, w1);
+        load_w(w1, min(i + 5, NL - 1));
+        run_step(i + 2, w2);
+        load_w(w2, min(i + 6, NL - 1));
+        run_step(i + 3, w3);
+        load_w(w3, min(i + 7, NL - 1));
+    }
+    if (NL - nfull > 0) run_step(nfull, w0);
+    if (NL - nfull > 1) run_step(nfull + 1, w1);
+    if (NL - nfull > 2) run_step(nfull + 2, w2);
+    if (mode != 0 && losses && step_no >= 1 && step_no <= loss_len && tid < HV) {
+        const int b = u0 + tid;
+        if (b < Bn) losses[(size_t)(step_no - 1) * Bn + b] = LS[tid];
+    }
+
+    if (mode == 0) {
+        for (int idx = tid; idx < D * HV; idx += blockDim.x) {
+            const int d = idx / HV, u = idx - d * HV;
+            const int b = u0 + u;
+            if (b < Bn) A.emb_out[(size_t)b * D + d] = EMB[d][u];
+        }
+        return;
+    }
+    for (int idx = tid; idx < C * HV; idx += blockDim.x) {
+        const int c = idx / HV, u = idx - c * HV;
+        const int b = u0 + u;
+        if (b < Bn) A.g_pooled[(size_t)b * C + c] = GB[c][u];
+    }
+}
+
 __global__ void attack_init(const float* __restrict__ vc, const float* __restrict__ ptb0, float* ptb, float* m,
                             float* v, float* adv, float eps, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -96,7 +96,7 @@ int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, cons
  *  LAYERED: one implicit-GEMM launch per Conv1d / dgrad over the whole batch, activations in HBM
  *           (any SpeakerEncoder config, any T).
  *  FUSED  : one workgroup per utterance runs the whole conv stack out of LDS (3 launches per
- *           iteration); needs c_in=80, c_h=c_bank=128, bank_scale=1, bank_size<=8, odd
+ *           iteration); needs c_in=80, c_h=c_bank=c_out=128, bank_scale=1, bank_size<=8, odd
  *           kernel_size<=5, <=8 conv blocks with subsample 1|2, and T<=128 (else LAYERED).
  * avc_set_engine fails (non-zero) if FUSED is requested for a config that cannot use it;
  * avc_get_engine returns the engine a call with T frames would run on. */
