@@ -26,7 +26,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
-from avc_native import context_for
+from avc_native import context_for, vc_context_for
 
 
 def _draw_ptb(vc_tgt: torch.Tensor) -> torch.Tensor:
@@ -58,13 +58,33 @@ def emb_attack(model: nn.Module, vc_tgt: torch.Tensor, adv_tgt: torch.Tensor, ep
     return out
 
 
+def _vc_attack(kind, model, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction, precision, return_info):
+    if ptb0 is None:
+        ptb0 = _draw_ptb(vc_tgt)
+    ctx = vc_context_for(model, vc_tgt.device)
+    out, losses, grad0 = ctx.vc_attack(kind, vc_src.detach().float(), vc_tgt.detach().float(),
+                                       adv_tgt.detach().float(), ptb0.detach().float(), eps, n_iters,
+                                       precision=precision, reduction=reduction,
+                                       want_losses=return_info, want_grad0=return_info)
+    out.requires_grad_(True)
+    if return_info:
+        return out, {"losses": losses, "grad0": grad0}
+    return out
+
+
 def e2e_attack(model: nn.Module, vc_src: torch.Tensor, vc_tgt: torch.Tensor, adv_tgt: torch.Tensor,
-               eps: float, n_iters: int, **kw):
-    """End-to-end attack (attack_utils.py:7-48)."""
-    raise NotImplementedError("e2e_attack: ContentEncoder/Decoder HIP path not built yet (see DESIGN.md 'next')")
+               eps: float, n_iters: int, *, ptb0: Optional[torch.Tensor] = None, reduction: str = "independent",
+               precision: str = "fp32", return_info: bool = False):
+    """End-to-end attack (attack_utils.py:7-48): perturb vc_tgt so that
+    inference(vc_src, vc_tgt + eps*tanh(ptb)) approaches inference(vc_src, adv_tgt) and
+    leaves inference(vc_src, vc_tgt).  Keyword extensions as emb_attack."""
+    return _vc_attack("e2e", model, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction, precision, return_info)
 
 
 def fb_attack(model: nn.Module, vc_src: torch.Tensor, vc_tgt: torch.Tensor, adv_tgt: torch.Tensor,
-              eps: float, n_iters: int, **kw):
-    """Feedback attack (attack_utils.py:89-130)."""
-    raise NotImplementedError("fb_attack: ContentEncoder/Decoder HIP path not built yet (see DESIGN.md 'next')")
+              eps: float, n_iters: int, *, ptb0: Optional[torch.Tensor] = None, reduction: str = "independent",
+              precision: str = "fp32", return_info: bool = False):
+    """Feedback attack (attack_utils.py:89-130): perturb vc_tgt so that
+    SpeakerEncoder(inference(vc_src, adv)) approaches SpeakerEncoder(adv_tgt) and leaves
+    SpeakerEncoder(inference(vc_src, vc_tgt)).  Keyword extensions as emb_attack."""
+    return _vc_attack("fb", model, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction, precision, return_info)

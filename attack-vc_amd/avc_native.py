@@ -30,6 +30,18 @@ class SECfg(ctypes.Structure):
                 ("subsample", ctypes.c_int32 * MAX_BLOCKS), ("act", ctypes.c_int32)]
 
 
+class VCCfg(ctypes.Structure):
+    _fields_ = [("ce_c_in", ctypes.c_int32), ("ce_c_h", ctypes.c_int32), ("ce_c_out", ctypes.c_int32),
+                ("ce_kernel_size", ctypes.c_int32), ("ce_bank_size", ctypes.c_int32),
+                ("ce_bank_scale", ctypes.c_int32), ("ce_c_bank", ctypes.c_int32),
+                ("ce_n_conv_blocks", ctypes.c_int32), ("ce_subsample", ctypes.c_int32 * MAX_BLOCKS),
+                ("ce_act", ctypes.c_int32),
+                ("dec_c_in", ctypes.c_int32), ("dec_c_cond", ctypes.c_int32), ("dec_c_h", ctypes.c_int32),
+                ("dec_c_out", ctypes.c_int32), ("dec_kernel_size", ctypes.c_int32),
+                ("dec_n_conv_blocks", ctypes.c_int32), ("dec_upsample", ctypes.c_int32 * MAX_BLOCKS),
+                ("dec_act", ctypes.c_int32)]
+
+
 class AttackOpts(ctypes.Structure):
     _fields_ = [("precision", ctypes.c_int32), ("reduction", ctypes.c_int32),
                 ("use_graph", ctypes.c_int32), ("losses", ctypes.c_void_p),
@@ -50,6 +62,17 @@ SIGNATURES = [
     ("avc_emb_attack", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_vc_weight_count", ctypes.c_size_t, [ctypes.POINTER(VCCfg)]),
+    ("avc_attach_vc", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(VCCfg), ctypes.c_void_p, ctypes.c_size_t]),
+    ("avc_vc_out_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("avc_inference", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_e2e_attack", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_fb_attack", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
     ("avc_set_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_get_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -165,6 +188,59 @@ class Context:
                                         ctypes.byref(o), ctypes.c_void_p(stream)))
         return out, losses, grad0
 
+    # --- voice-conversion path (ContentEncoder + Decoder) ----------------------------
+    def attach_vc(self, ce_cfg: Dict, dec_cfg: Dict, flat: torch.Tensor):
+        """Hand the ContentEncoder / Decoder weights (content_encoder.* then decoder.*,
+        state_dict order) to libavc (avc_attach_vc)."""
+        self._vcs = vc_cfg_struct(ce_cfg, dec_cfg)
+        w = flat.detach().to("cpu", torch.float32).contiguous()
+        need = lib().avc_vc_weight_count(ctypes.byref(self._vcs))
+        if w.numel() != need:
+            raise RuntimeError(f"ContentEncoder/Decoder weights: got {w.numel()} values, config needs {need}")
+        _check(lib().avc_attach_vc(self.h, ctypes.byref(self._vcs), ctypes.c_void_p(w.data_ptr()), w.numel()))
+
+    def vc_out_frames(self, T: int) -> int:
+        n = lib().avc_vc_out_frames(self.h, int(T))
+        if n < 0:
+            raise RuntimeError(lib().avc_last_error().decode(errors="replace"))
+        return n
+
+    def inference(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
+        _require_gpu(src, tgt)
+        src, tgt = src.contiguous(), tgt.contiguous()
+        if src.shape != tgt.shape or src.dim() != 3:
+            raise RuntimeError(f"inference: src {tuple(src.shape)} and tgt {tuple(tgt.shape)} must be equal [B, 80, T]")
+        B, C, T = src.shape
+        out = torch.empty(B, 80, self.vc_out_frames(T), device=src.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream(src.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_inference(self.h, ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(tgt.data_ptr()),
+                                       B, T, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+        return out
+
+    def vc_attack(self, kind: str, vc_src, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
+                  reduction="independent", use_graph=True, want_losses=False, want_grad0=False):
+        """kind "e2e" (avc_e2e_attack) or "fb" (avc_fb_attack)."""
+        _require_gpu(vc_src, vc_tgt, adv_tgt, ptb0)
+        vc_src, vc_tgt, adv_tgt, ptb0 = (t.contiguous() for t in (vc_src, vc_tgt, adv_tgt, ptb0))
+        if not (vc_src.shape == vc_tgt.shape == adv_tgt.shape == ptb0.shape) or vc_tgt.dim() != 3:
+            raise RuntimeError(f"shape mismatch: vc_src {tuple(vc_src.shape)}, vc_tgt {tuple(vc_tgt.shape)}, "
+                               f"adv_tgt {tuple(adv_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
+        B, C, T = vc_tgt.shape
+        out = torch.empty_like(vc_tgt)
+        losses = torch.empty(n_iters, B, device=vc_tgt.device) if want_losses and n_iters > 0 else None
+        grad0 = torch.empty_like(vc_tgt) if want_grad0 and n_iters > 0 else None
+        o = AttackOpts(PREC[precision], REDUCE[reduction], 1 if use_graph else 0,
+                       losses.data_ptr() if losses is not None else None,
+                       grad0.data_ptr() if grad0 is not None else None)
+        fn = {"e2e": lib().avc_e2e_attack, "fb": lib().avc_fb_attack}[kind]
+        stream = torch.cuda.current_stream(vc_tgt.device).cuda_stream
+        with self._lock:
+            _check(fn(self.h, ctypes.c_void_p(vc_src.data_ptr()), ctypes.c_void_p(vc_tgt.data_ptr()),
+                      ctypes.c_void_p(adv_tgt.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()), B, T, float(eps),
+                      int(n_iters), ctypes.c_void_p(out.data_ptr()), ctypes.byref(o), ctypes.c_void_p(stream)))
+        return out, losses, grad0
+
     def set_engine(self, engine: str = "auto"):
         """"auto" | "layered" | "fused" (include/avc.h AVC_ENGINE_*)."""
         _check(lib().avc_set_engine(self.h, ENGINE[engine]))
@@ -210,6 +286,49 @@ def se_config(se: torch.nn.Module) -> Dict:
                 subsample=list(se.subsample), act=act)
 
 
+def vc_cfg_struct(ce: Dict, dec: Dict) -> VCCfg:
+    s = VCCfg()
+    for k in ("c_in", "c_h", "c_out", "kernel_size", "bank_size", "bank_scale", "c_bank", "n_conv_blocks", "act"):
+        setattr(s, "ce_" + k, int(ce[k]))
+    for k in ("c_in", "c_cond", "c_h", "c_out", "kernel_size", "n_conv_blocks", "act"):
+        setattr(s, "dec_" + k, int(dec[k]))
+    sub = list(ce["subsample"])[: int(ce["n_conv_blocks"])]
+    ups = list(dec["upsample"])[: int(dec["n_conv_blocks"])]
+    if len(sub) > MAX_BLOCKS or len(ups) > MAX_BLOCKS:
+        raise RuntimeError(f"at most {MAX_BLOCKS} conv blocks supported")
+    for i, v in enumerate(sub):
+        s.ce_subsample[i] = int(v)
+    for i, v in enumerate(ups):
+        s.dec_upsample[i] = int(v)
+    return s
+
+
+def _act_of(mod) -> int:
+    return 1 if isinstance(getattr(mod, "act", None), torch.nn.LeakyReLU) else 0
+
+
+def ce_config(ce: torch.nn.Module) -> Dict:
+    """Hyper-parameters of a ContentEncoder (ours or the reference's, models.py:121-179)."""
+    if hasattr(ce, "avc_config"):
+        return ce.avc_config()
+    ks = [m.kernel_size[0] for m in ce.conv_bank]
+    return dict(c_in=ce.conv_bank[0].in_channels, c_h=ce.in_conv_layer.out_channels,
+                c_out=ce.mean_layer.out_channels, kernel_size=ce.first_conv_layers[0].kernel_size[0],
+                bank_size=ks[-1], bank_scale=ks[1] - ks[0] if len(ks) > 1 else ks[0],
+                c_bank=ce.conv_bank[0].out_channels, n_conv_blocks=ce.n_conv_blocks,
+                subsample=list(ce.subsample), act=_act_of(ce))
+
+
+def dec_config(dec: torch.nn.Module) -> Dict:
+    """Hyper-parameters of a Decoder (ours or the reference's, models.py:346-401)."""
+    if hasattr(dec, "avc_config"):
+        return dec.avc_config()
+    return dict(c_in=dec.in_conv_layer.in_channels, c_cond=dec.conv_affine_layers[0].in_features,
+                c_h=dec.in_conv_layer.out_channels, c_out=dec.out_conv_layer.out_channels,
+                kernel_size=dec.first_conv_layers[0].kernel_size[0], n_conv_blocks=dec.n_conv_blocks,
+                upsample=list(dec.upsample), act=_act_of(dec))
+
+
 def context_for(se: torch.nn.Module, device: torch.device) -> Context:
     """Cached libavc context for this speaker encoder's current weights on `device`."""
     if device.type != "cuda":
@@ -229,3 +348,17 @@ def speaker_encoder_forward(se: torch.nn.Module, x: torch.Tensor) -> torch.Tenso
     """SpeakerEncoder.forward (models.py:327-343) on the MI355X; no autograd."""
     _require_gpu(x)
     return context_for(se, x.device).se_forward(x)
+
+
+def vc_context_for(model: torch.nn.Module, device: torch.device) -> Context:
+    """Context of model.speaker_encoder with model.content_encoder / model.decoder attached
+    (re-attached whenever their parameters change)."""
+    ctx = context_for(model.speaker_encoder, device)
+    mods = (model.content_encoder, model.decoder)
+    version = tuple((p.data_ptr(), p._version) for m in mods for p in m.parameters())
+    if getattr(ctx, "_vc_version", None) != version:
+        flat = torch.cat([v.detach().reshape(-1).to("cpu", torch.float32)
+                          for m in mods for v in m.state_dict().values()])
+        ctx.attach_vc(ce_config(model.content_encoder), dec_config(model.decoder), flat)
+        ctx._vc_version = version
+    return ctx

@@ -5,10 +5,12 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -28,6 +30,11 @@ template <int PREC, int SH>
 __global__ void se_fwd_fused(FusedArgs A);
 template <int PREC, int SH>
 __global__ void se_bwd_fused(FusedArgs A);
+template <int PREC, int SH>
+__global__ void dec_fwd_fused(DecArgs A);
+template <int PREC, int SH>
+__global__ void dec_bwd_fused(DecArgs A);
+__global__ void dense_batched(DenseArgs D);
 }  // namespace avc
 #include "avc_fused_lds.h"
 
@@ -69,7 +76,7 @@ struct HostConv {
     const float* b;
 };
 
-enum LaunchKind { L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD };
+enum LaunchKind { L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD, L_DZ_FWD, L_DZ_BWD, L_DENSE };
 
 // conv_gemm instantiations (avc_gemm_variants.h); the planner autotunes one per
 // launch and precision on first use of a workspace.
@@ -102,6 +109,8 @@ struct Launch {
     HeadArgs head{};
     FusedArgs fz{};              // L_FZ_*: per-utterance fused SpeakerEncoder pass (prec = PREC_*)
     int fz_shape = 8;            // L_FZ_*: kernel shape SH (0 = standard config at T = 128, else 1|2|4|8)
+    DecArgs dz{};                // L_DZ_*: per-utterance fused Decoder pass (shape: fz_shape 0 | 8)
+    DenseArgs dn{};              // L_DENSE: batched conv_affine layer (or its transpose)
     double flop = 0;             // algorithmic FLOPs of this launch
     std::string name;
 };
@@ -126,11 +135,16 @@ struct Workspace {
     Plan fwd, iter, iter_bf16;
     hipGraphExec_t graph = nullptr, graph_bf16 = nullptr;
     bool built = false;
+    int gen = 0;                      // bumped whenever buffers / plans are rebuilt
 };
 
 }  // namespace
 
+struct VcState;   // ContentEncoder + Decoder of the e2e / fb attacks (avc_vc_host.inc)
+static void vc_free(avc_ctx* ctx);
+
 struct avc_ctx {
+    VcState* vc = nullptr;
     int device = 0;
     avc_se_cfg cfg{};
     int nb = 0;                         // bank kernels
@@ -148,7 +162,7 @@ struct avc_ctx {
     DevBuf head_Wr, head_WrT;           // se_head_v: row-major dense/output weights and transposes
     bool fused_ok = false;              // config fits the fused per-utterance engine
     int engine = AVC_ENGINE_AUTO;       // avc_set_engine
-    std::vector<DevBuf> fz_bufs;        // packed fused-engine A operands (both precisions)
+    std::deque<DevBuf> fz_bufs;         // packed fused-engine A operands (both precisions)
     FusedW fzw[2];                      // [PREC_F32], [PREC_BF16]
     std::map<const float*, void*> bf16_of;   // fp32 A matrix -> its bf16 copy (device)
     hipStream_t stream = nullptr;
@@ -332,13 +346,20 @@ static int fz_pack(avc_ctx* ctx, int prec, int M, int K, G get, const void*& dst
     return 0;
 }
 
-static int pack_fused(avc_ctx* ctx, const std::vector<HostConv>& bank, const HostConv& inc,
-                      const std::vector<HostConv>& c1, const std::vector<HostConv>& c2) {
-    const avc_se_cfg& c = ctx->cfg;
-    const int nb = ctx->nb, C = FZ_C, CI = FZ_CIN, ks = c.kernel_size, cat = inc.ci;
-    ctx->fz_bufs.reserve(2 * (4 * nb + 2 + 4 * c.n_conv_blocks));
+// device bias pointers of one fused encoder (SpeakerEncoder or ContentEncoder)
+struct FzBias {
+    std::vector<const float*> bank, c1, c2;
+    const float* in = nullptr;
+};
+
+// A operands of the fused encoder kernels in both precisions into dst[PREC_F32 / PREC_BF16]
+// (ctx->fz_bufs owns the device buffers; it is a std::deque, so earlier packs stay put)
+static int pack_fused(avc_ctx* ctx, FusedW* dst, const std::vector<HostConv>& bank, const HostConv& inc,
+                      const std::vector<HostConv>& c1, const std::vector<HostConv>& c2, const FzBias& fb) {
+    const int nb = (int)bank.size(), C = FZ_C, CI = FZ_CIN, ks = c1.empty() ? 1 : c1[0].k, cat = inc.ci;
+    const int nblk = (int)c1.size();
     for (int prec = 0; prec < 2; ++prec) {
-        FusedW& W = ctx->fzw[prec];
+        FusedW& W = dst[prec];
         int rc = 0;
         for (int kb = 0; kb < nb; ++kb) {
             const HostConv& q = bank[kb];
@@ -353,12 +374,12 @@ static int pack_fused(avc_ctx* ctx, const std::vector<HostConv>& bank, const Hos
             // bank^T: A[ci][j*128 + co] = W[co][ci][j]
             rc |= fz_pack(ctx, prec, CI, k * C, [&](int m, int kk) { return q.W[((size_t)(kk % C) * CI + m) * k + kk / C]; },
                           W.bankT[kb]);
-            W.b_bank[kb] = ctx->bias_bank[kb].p;
+            W.b_bank[kb] = fb.bank[kb];
         }
         rc |= fz_pack(ctx, prec, C, CI, [&](int m, int kk) { return inc.W[(size_t)m * cat + nb * C + kk]; }, W.in_x);
         rc |= fz_pack(ctx, prec, CI, C, [&](int m, int kk) { return inc.W[(size_t)kk * cat + nb * C + m]; }, W.inT_x);
-        W.b_in = ctx->bias_in.p;
-        for (int l = 0; l < c.n_conv_blocks; ++l) {
+        W.b_in = fb.in;
+        for (int l = 0; l < nblk; ++l) {
             for (int which = 0; which < 2; ++which) {
                 const HostConv& q = which ? c2[l] : c1[l];
                 const void*& f = which ? W.c2[l] : W.c1[l];
@@ -366,11 +387,15 @@ static int pack_fused(avc_ctx* ctx, const std::vector<HostConv>& bank, const Hos
                 rc |= fz_pack(ctx, prec, C, ks * C, [&](int m, int kk) { return q.W[((size_t)m * C + kk % C) * ks + kk / C]; }, f);
                 rc |= fz_pack(ctx, prec, C, ks * C, [&](int m, int kk) { return q.W[((size_t)(kk % C) * C + m) * ks + kk / C]; }, t);
             }
-            W.b_c1[l] = ctx->bias_c1[l].p;
-            W.b_c2[l] = ctx->bias_c2[l].p;
+            W.b_c1[l] = fb.c1[l];
+            W.b_c2[l] = fb.c2[l];
         }
         if (rc) return 1;
     }
+    return 0;
+}
+
+static int set_fused_attrs() {
     // every fused kernel needs more than the default 64 KiB of dynamic LDS
 #define AVC_FZ_FNS(SH)                                                                      \
     {(const void*)se_fwd_fused<PREC_F32, SH>, fz_lds_fwd(PREC_F32, 128, 5)},                \
@@ -543,7 +568,17 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
         up(ctx->head_WrT, WrT);
     }
     ctx->fused_ok = fused_cfg_ok(c);
-    if (!rc && ctx->fused_ok) rc |= pack_fused(ctx, bank, inc, c1, c2);
+    if (!rc && ctx->fused_ok) {
+        FzBias fb;
+        for (int i = 0; i < nb; ++i) fb.bank.push_back(ctx->bias_bank[i].p);
+        for (int l = 0; l < c.n_conv_blocks; ++l) {
+            fb.c1.push_back(ctx->bias_c1[l].p);
+            fb.c2.push_back(ctx->bias_c2[l].p);
+        }
+        fb.in = ctx->bias_in.p;
+        rc |= pack_fused(ctx, ctx->fzw, bank, inc, c1, c2, fb);
+        rc |= set_fused_attrs();
+    }
     if (rc) {
         avc_destroy(ctx);
         return 1;
@@ -604,6 +639,7 @@ extern "C" void avc_destroy(avc_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    vc_free(ctx);
     free_ws(ctx->ws);
     for (auto* v : {&ctx->AtF_bank, &ctx->AtF_c1, &ctx->AtF_c2, &ctx->AtB_c1, &ctx->AtB_c2, &ctx->bias_bank,
                     &ctx->bias_c1, &ctx->bias_c2})
@@ -1175,6 +1211,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     ws.iters_cap = cap;
     // (re)build plans: pointers may have moved (the bf16 plan is rebuilt on demand)
     free_plans(ws);
+    ++ws.gen;
     if (ws.fused) {
         if (plan_fused_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return 1;
     } else {
@@ -1272,6 +1309,20 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
         klaunch(ev, false, k, L.grid, L.block, L.shmem, s, L.fz);
         return hipGetLastError();
     }
+    case L_DZ_FWD:
+    case L_DZ_BWD: {
+        typedef void (*DzK)(DecArgs);
+#define AVC_DZ_K(SH)                                                                                   \
+    (L.kind == L_DZ_FWD ? (L.prec == PREC_F32 ? (DzK)dec_fwd_fused<PREC_F32, SH> : (DzK)dec_fwd_fused<PREC_BF16, SH>) \
+                        : (L.prec == PREC_F32 ? (DzK)dec_bwd_fused<PREC_F32, SH> : (DzK)dec_bwd_fused<PREC_BF16, SH>))
+        const DzK k = L.fz_shape == 0 ? AVC_DZ_K(0) : AVC_DZ_K(8);
+#undef AVC_DZ_K
+        klaunch(ev, false, k, L.grid, L.block, L.shmem, s, L.dz);
+        return hipGetLastError();
+    }
+    case L_DENSE:
+        klaunch(ev, false, dense_batched, L.grid, L.block, 0, s, L.dn);
+        return hipGetLastError();
     default:
         return hipErrorInvalidValue;
     }
@@ -1596,3 +1647,5 @@ extern "C" int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len,
     if (total_flop) *total_flop = it->second.second;
     return 0;
 }
+
+#include "avc_vc_host.inc"

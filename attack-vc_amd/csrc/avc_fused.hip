@@ -36,351 +36,9 @@
 // The residual stream h and its gradient stay fp32 in registers in the MFMA C/D
 // layout (col = lane&15, row = 4*(lane>>4)+reg); avg_pool1d(ceil_mode) and its
 // adjoint are lane shuffles.  Only the bf16/fp32 operand copies go through LDS.
-#include <hip/hip_runtime.h>
-
-#include <type_traits>
-
-#include "avc_device.h"
-#include "avc_kernels.h"
-#include "avc_fused_lds.h"
+#include "avc_fused_core.h"
 
 namespace avc {
-
-template <int PREC>
-struct Fz;
-template <>
-struct Fz<PREC_F32> {
-    using E = float;
-    static constexpr int RS = 544;    // 128 ch * 4 B + 32 B
-};
-template <>
-struct Fz<PREC_BF16> {
-    using E = __bf16;
-    static constexpr int RS = 288;    // 128 ch * 2 B + 32 B
-};
-
-extern __shared__ __attribute__((aligned(16))) char fz_lds[];
-
-#ifndef AVC_FZ_ABLATE          // timing experiments only: 1 = no A loads, 2 = no mask bookkeeping
-#define AVC_FZ_ABLATE 0
-#endif
-
-typedef unsigned long long u64;
-
-
-__device__ __forceinline__ f32x4 lds16(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
-
-template <int PREC>
-__device__ __forceinline__ void st4(char* p, f32x4 v) {
-    if constexpr (PREC == PREC_F32) {
-        *reinterpret_cast<f32x4*>(p) = v;
-    } else {
-        bf16x4 b;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
-        *reinterpret_cast<bf16x4*>(p) = b;
-    }
-}
-
-template <int PREC>
-__device__ __forceinline__ void st1(char* p, float v) {
-    *reinterpret_cast<typename Fz<PREC>::E*>(p) = (typename Fz<PREC>::E)v;
-}
-
-template <int PREC>
-__device__ __forceinline__ void mma(f32x4& acc, const f32x4& a, const f32x4& b) {
-    if constexpr (PREC == PREC_F32) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], b[e], acc, 0, 0, 0);
-    } else {
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
-                                                      acc, 0, 0, 0);
-    }
-}
-
-template <int MT, int NF>
-__device__ __forceinline__ void zero_acc(f32x4 (&acc)[MT][NF]) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int f = 0; f < NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-}
-
-// ---------------------------------------------------------------------------------
-// A operands and the cross-GEMM prefetch ring
-// ---------------------------------------------------------------------------------
-// One GEMM's A as seen by this wave: packed base at the wave's first M tile (lane offset
-// applied), mt own tiles amt f32x4 apart, ns K steps with the step map
-// ps = (s >> lg)*spt + soff + (s & msk) (identity, or a K-split over waves).
-struct AOp {
-    const f32x4* p;
-    int amt, mt, ns, lg, msk, spt, soff;
-};
-__device__ __forceinline__ AOp aop(const void* packed, int tile0, int mt, int nst, int ns, int lg = 30, int msk = -1,
-                                   int spt = 0, int soff = 0) {
-    AOp o;
-    o.p = reinterpret_cast<const f32x4*>(packed) + (size_t)tile0 * nst * 64 + (threadIdx.x & 63);
-    o.amt = nst * 64;
-    o.mt = mt;
-    o.ns = ns;
-    o.lg = lg;
-    o.msk = msk;
-    o.spt = spt;
-    o.soff = soff;
-    return o;
-}
-__device__ __forceinline__ const f32x4* a_step(const AOp& o, int s) {
-    s = s < o.ns ? s : o.ns - 1;
-    return o.p + (size_t)((s >> o.lg) * o.spt + o.soff + (s & o.msk)) * 64;
-}
-// Four K steps of A in flight: slot u of the ring holds step s+u.  A GEMM refills a slot
-// right after using it, and the refills that run past its last step fetch the NEXT
-// GEMM's first steps instead, so no GEMM starts with an exposed L2/MALL round trip.
-template <int MTR>
-struct ARing {
-    f32x4 a[4][MTR];
-};
-// slot <- step s of A (s < A.ns) or step s - A.ns of N; branch-free (uniform selects);
-// tiles beyond an operand's own count re-read its last tile (an L1 hit, never used)
-template <int MTR>
-__device__ __forceinline__ void ring_load(f32x4 (&slot)[MTR], const AOp& A, const AOp& N, int s) {
-#if AVC_FZ_ABLATE & 4
-    const bool own = true;   // debug: no cross-GEMM prefetch (N's steps loaded as A's last)
-#else
-    const bool own = s < A.ns;
-#endif
-    const f32x4* base = own ? a_step(A, s) : a_step(N, s - A.ns > 0 ? s - A.ns : 0);
-    const int amt = own ? A.amt : N.amt;
-    const int mt = own ? A.mt : N.mt;
-#pragma unroll
-    for (int i = 0; i < MTR; ++i)
-        slot[i] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
-            (const __attribute__((address_space(1))) f32x4*)(base + (size_t)(i < mt ? i : mt - 1) * amt));
-#if AVC_FZ_ABLATE & 1
-#pragma unroll
-    for (int i = 0; i < MTR; ++i) slot[i] = f32x4{0.001f * s, 0.f, 0.f, 0.f};
-#endif
-}
-template <int MTR>
-__device__ __forceinline__ void ring_fill(ARing<MTR>& R, const AOp& A) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) ring_load<MTR>(R.a[u], A, A, u);
-}
-
-// acc[MT][NF] += A x B; the ring holds A's steps 0..3 on entry and N's steps 0..3 on exit.
-//   B  : LDS base of the operand image; rb[f] = row of tap 0 for this lane's column
-//   DJ : +1 forward (row = rb + j), -1 adjoint (row = rb - j)
-// B fragments are read one step ahead into two alternating register sets.  The loop
-// body has no early exits and issues every load unconditionally (steps past the end
-// are clamped), so accumulators keep their registers across the back edge and the
-// waitcnt pass sees a fixed number of loads in flight.
-// NFC > 0: the live fragment count is the compile-time NFC (straight-line K loop);
-// NFC == 0: up to NF fragments, the first `nf` live (runtime guards; generic shapes).
-template <int PREC, int MT, int MTR, int NF, int NFC, int CINB, int DJ>
-__device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing<MTR>& R, const AOp& A,
-                                             const AOp& N, const char* B, const int (&rb)[NF]) {
-    static_assert(MT <= MTR, "ring narrower than the GEMM");
-    constexpr int NL = NFC ? NFC : NF;                 // fragments the loops run over
-    auto live = [&](int f) __attribute__((always_inline)) { return NFC ? f < NFC : f < nf; };
-    using E = typename Fz<PREC>::E;
-    constexpr int RS = Fz<PREC>::RS;
-    constexpr int VE = 16 / (int)sizeof(E);
-    constexpr int KS = 4 * VE;
-    const int kq = (threadIdx.x & 63) >> 4;
-    const int ns = A.ns;
-    int rbo[NL];
-#pragma unroll
-    for (int f = 0; f < NL; ++f) rbo[f] = rb[f] * RS;
-    auto read_b = [&](f32x4 (&b)[NL], int s) __attribute__((always_inline)) {
-        s = s < ns ? s : ns - 1;
-        const int kl = KS * ((s >> A.lg) * A.spt + A.soff + (s & A.msk)) + VE * kq;
-        const int j = kl / CINB;
-        const int ci = kl - j * CINB;
-        const char* Bs = B + ci * (int)sizeof(E) + DJ * j * RS;
-#pragma unroll
-        for (int f = 0; f < NL; ++f)
-            if (live(f)) b[f] = lds16(Bs + rbo[f]);
-    };
-    auto mma_all = [&](const f32x4 (&a)[MTR], const f32x4 (&b)[NL]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int f = 0; f < NL; ++f)
-                if (live(f)) mma<PREC>(acc[i][f], a[i], b[f]);
-    };
-    f32x4 bA[NL], bB[NL];
-    read_b(bA, 0);
-    const int nfull = ns & ~3;
-#pragma unroll 1
-    for (int s = 0; s < nfull; s += 4) {
-        read_b(bB, s + 1);
-        mma_all(R.a[0], bA);
-        ring_load<MTR>(R.a[0], A, N, s + 4);
-        read_b(bA, s + 2);
-        mma_all(R.a[1], bB);
-        ring_load<MTR>(R.a[1], A, N, s + 5);
-        read_b(bB, s + 3);
-        mma_all(R.a[2], bA);
-        ring_load<MTR>(R.a[2], A, N, s + 6);
-        read_b(bA, s + 4);
-        mma_all(R.a[3], bB);
-        ring_load<MTR>(R.a[3], A, N, s + 7);
-    }
-    // remainder (0..3 steps): slots hold steps nfull..nfull+3 (slot u = step nfull+u),
-    // bA holds step nfull.  Afterwards rotate so that slot u = N's step u again.
-    const int rem = ns - nfull;
-#if AVC_FZ_ABLATE & 4
-    // debug: no cross-GEMM prefetch -- finish this GEMM's own steps, then load N afresh
-    if (rem >= 1) mma_all(R.a[0], bA);
-    if (rem >= 2) {
-        read_b(bB, nfull + 1);
-        mma_all(R.a[1], bB);
-    }
-    if (rem >= 3) {
-        read_b(bA, nfull + 2);
-        mma_all(R.a[2], bA);
-    }
-    ring_fill(R, N);
-    return;
-#endif
-    if (rem == 0) return;
-    mma_all(R.a[0], bA);
-    ring_load<MTR>(R.a[0], A, N, nfull + 4);
-    if (rem >= 2) {
-        read_b(bB, nfull + 1);
-        mma_all(R.a[1], bB);
-        ring_load<MTR>(R.a[1], A, N, nfull + 5);
-    }
-    if (rem >= 3) {
-        read_b(bA, nfull + 2);
-        mma_all(R.a[2], bA);
-        ring_load<MTR>(R.a[2], A, N, nfull + 6);
-    }
-    // a GEMM shorter than the ring (ns < 4) entered with slots u >= ns holding clamped
-    // copies of its own last step (its predecessor could not know this GEMM's successor):
-    // those slots get N's steps u - rem now
-    if (nfull == 0)
-        for (int u = rem; u < 4; ++u) {
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-                if (v == u) ring_load<MTR>(R.a[v], N, N, u - rem);
-        }
-    // slot u now holds step nfull + u + 4*(u < rem) of the A|N stream, i.e. N's step
-    // (u - rem) mod 4: rotate left by rem
-    f32x4 t[4][MTR];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < MTR; ++i) t[u][i] = R.a[u][i];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < MTR; ++i)
-            R.a[u][i] = rem == 1 ? t[(u + 1) & 3][i] : (rem == 2 ? t[(u + 2) & 3][i] : t[(u + 3) & 3][i]);
-}
-
-template <int V>
-using IC = std::integral_constant<int, V>;
-
-// fz_gemm: the fragment count is either a compile-time IC<N> (specialised shapes) or a
-// runtime int (generic shapes)
-template <int PREC, int MT, int NF, int CINB, int DJ, int MTR, int NFC>
-__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], IC<NFC>, ARing<MTR>& R, const AOp& A, const AOp& N,
-                                        const char* B, const int (&rb)[NF]) {
-    static_assert(NFC >= 1 && NFC <= NF, "fragment count");
-    fz_gemm_impl<PREC, MT, MTR, NF, NFC, CINB, DJ>(acc, NFC, R, A, N, B, rb);
-}
-template <int PREC, int MT, int NF, int CINB, int DJ, int MTR>
-__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], int nf, ARing<MTR>& R, const AOp& A, const AOp& N,
-                                        const char* B, const int (&rb)[NF]) {
-    fz_gemm_impl<PREC, MT, MTR, NF, 0, CINB, DJ>(acc, nf, R, A, N, B, rb);
-}
-
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(IC<I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
-// position of dgrad output column n in input coordinates: interior n < Tin -> n;
-// then E left pad positions -E..-1, then E right pad positions Tin..Tin+E-1
-__device__ __forceinline__ int vpos(int n, int Tin, int E) {
-    return n < Tin ? n : (n < Tin + E ? n - Tin - E : n - E);
-}
-
-// reflect-pad adjoint on the accumulators: the sum at pad position v folds onto
-// interior frame -v (left) or 2(Tin-1)-v (right)   (F.pad mode="reflect", models.py:23-29).
-// Edge column e (n = Tin + e) is staged through this wave's LDS scratch [MT*16 ch][8]
-// and pulled by its target lane: fragment indices stay compile-time (no dynamic
-// register indexing).  Called by all waves at the same point (contains a barrier).
-template <int MT, int NF>
-__device__ __forceinline__ void fold_edges(f32x4 (&acc)[MT][NF], int Tin, int E, float* scr) {
-    const int lane = threadIdx.x & 63, c = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-        const int e = 16 * f + c - Tin;
-        if (e >= 0 && e < 2 * E) {
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) scr[(16 * i + 4 * kq + r) * 8 + e] = acc[i][f][r];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < NF; ++g) {
-        const int t = 16 * g + c;
-        const int el = (t >= 1 && t <= E) ? E - t : -1;                          // v = -t
-        const int er = (t >= Tin - 1 - E && t <= Tin - 2) ? Tin - 2 - t + E : -1; // v = 2(Tin-1)-t
-        if (el >= 0 || er >= 0) {
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float* row = scr + (16 * i + 4 * kq + r) * 8;
-                    float add = el >= 0 ? row[el] : 0.f;
-                    if (er >= 0) add += row[er];
-                    acc[i][g][r] += add;
-                }
-        }
-    }
-}
-
-// 64-bit ReLU' ballot words of one layer for this wave: word (i*FZ_MAXNF + f)*4 + r
-// lives in lane word%64 of lo (words < 64) or hi (words >= 64)
-struct MaskAcc {
-    u64 lo = 0, hi = 0;
-    __device__ __forceinline__ void put(int widx, u64 word) {
-        if (AVC_FZ_ABLATE & 2) return;
-        const int lane = threadIdx.x & 63;
-        if (widx < 64) {
-            if (lane == widx) lo = word;
-        } else {
-            if (lane == widx - 64) hi = word;
-        }
-    }
-    __device__ __forceinline__ void store(u64* base) const {
-        const int lane = threadIdx.x & 63;
-        base[lane] = lo;
-        if (lane < FZ_MASK_WORDS_PER_LAYER / 4 - 64) base[64 + lane] = hi;
-    }
-};
-
-__device__ __forceinline__ float act_bit(u64 word, int lane, int act) {
-    return ((word >> lane) & 1ull) ? 1.f : (act ? 0.01f : 0.f);
-}
-
-// write 4 consecutive channels of frame t of a padded operand image (pad P rows each
-// side, reflect): row P+t, plus its mirror rows (F.pad reflect)
-template <int PREC>
-__device__ __forceinline__ void put_reflect(char* img, int t, int T, int P, int chbyte, f32x4 v) {
-    constexpr int RS = Fz<PREC>::RS;
-    st4<PREC>(img + (P + t) * RS + chbyte, v);
-    if (t >= 1 && t <= P) st4<PREC>(img + (P - t) * RS + chbyte, v);
-    if (t >= T - 1 - P && t <= T - 2) st4<PREC>(img + (P + 2 * T - 2 - t) * RS + chbyte, v);
-}
 
 // ---------------------------------------------------------------------------------
 // shapes (kernel template parameter SH):
@@ -435,8 +93,9 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     char* HB = fz_lds;                                  // block input image [T+2P][128]
     char* YB = HB + (T + 2 * P) * RS;                   // conv1 output image
 
+    const bool ce = A.ce_mode != 0;                     // ContentEncoder pass
     u64* mbase = A.masks + (size_t)b * A.mask_words;
-    const bool wm = A.write_masks != 0;
+    const bool wm = A.write_masks != 0 && !ce;
     const int ch0 = 32 * w + 4 * kq;                    // + 16*i + r
     constexpr int WPL = FZ_MASK_WORDS_PER_LAYER / 4;    // mask words per (layer, wave)
 
@@ -467,6 +126,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     };
     auto op_c1 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1[l], 2 * w, 2, ns_c, ns_c); };
     auto op_c2 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_mean = [&]() __attribute__((always_inline)) { return aop(A.w.mean_w, 2 * w, 2, FZ_C / KS, FZ_C / KS); };
     ARing<2> ring;
     ring_fill(ring, op_bank(0));
     int rb[NF];
@@ -523,11 +183,20 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         for (int i = 0; i < 2; ++i) {
             const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_in + ch0 + 16 * i);
 #pragma unroll
+            for (int f = 0; f < NF; ++f) acc_h[i][f] += bi;
+        }
+        if (ce) {   // ContentEncoder: InstanceNorm before the act (models.py:199-200)
+            f32x4 is[2];
+            inorm_rows(acc_h, nf0, T, is);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
             for (int f = 0; f < NF; ++f) {
                 f32x4 y;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    y[r] = act_f(acc_h[i][f][r] + bi[r], act);
+                    y[r] = act_f(acc_h[i][f][r], act);
                     mk.put((i * FZ_MAXNF + f) * 4 + r, __ballot(y[r] > 0.f));
                 }
                 hres[i][f] = y;
@@ -552,12 +221,21 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         for (int i = 0; i < 2; ++i) {
             const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_c1[l] + ch0 + 16 * i);
 #pragma unroll
+            for (int f = 0; f < NF; ++f) acc[i][f] += bi;
+        }
+        if (ce) {
+            f32x4 is[2];
+            inorm_rows(acc, nfi, Ti, is);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
             for (int f = 0; f < NF; ++f) {
                 if (f >= nfi) continue;
                 f32x4 y;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    y[r] = act_f(acc[i][f][r] + bi[r], act);
+                    y[r] = act_f(acc[i][f][r], act);
                     mk.put((i * FZ_MAXNF + f) * 4 + r, __ballot(y[r] > 0.f));
                 }
                 const int t = 16 * f + c;
@@ -570,7 +248,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         zero_acc(acc);
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, To - 1) * s;
-        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfo, ring, op_c2(l), l + 1 < nblk ? op_c1(l + 1) : op_c2(l), YB, rb);
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfo, ring, op_c2(l),
+                                      l + 1 < nblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l)), YB, rb);
         if (s == 2) {
             // pooled[t'] = (h[2t'] + h[2t'+1]) / cnt : sources in frags 2f', 2f'+1; increasing f'
             // order keeps the in-place update safe (frag f' is read before it is written)
@@ -601,12 +280,21 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         for (int i = 0; i < 2; ++i) {
             const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_c2[l] + ch0 + 16 * i);
 #pragma unroll
+            for (int f = 0; f < NF; ++f) acc[i][f] += bi;
+        }
+        if (ce) {
+            f32x4 is[2];
+            inorm_rows(acc, nfo, To, is);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
             for (int f = 0; f < NF; ++f) {
                 if (f >= nfo) continue;
                 f32x4 y, h;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    y[r] = act_f(acc[i][f][r] + bi[r], act);
+                    y[r] = act_f(acc[i][f][r], act);
                     mk.put((i * FZ_MAXNF + f) * 4 + r, __ballot(y[r] > 0.f));
                     h[r] = y[r] + hres[i][f][r];
                 }
@@ -632,6 +320,27 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         TN = A.Tl[A.nblk];
     }
 
+    if (ce) {
+        // mean_layer (1x1, models.py:207): mu = W_mean h_N + b over the TN frames of HB
+        f32x4 acc[2][NF];
+        zero_acc(acc);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) rb[f] = P + min(16 * f + c, TN - 1);
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nf0, ring, op_mean(), op_mean(), HB, rb);
+        float* mu = A.mu_out + (size_t)b * FZ_C * TN;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_mean + ch0 + 16 * i);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = 16 * f + c;
+                if (t < TN)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) mu[(size_t)(ch0 + 16 * i + r) * TN + t] = acc[i][f][r] + bi[r];
+            }
+        }
+        return;
+    }
     // AdaptiveAvgPool1d(1): mean over the TN frames of each channel
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -912,6 +621,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         __syncthreads();
     }
 
+    if (A.gx_out) {   // d loss / d x handed on (fb: the decoder output's gradient)
+        float* gx = A.gx_out + (size_t)b * FZ_CIN * T;
+        for (int idx = tid; idx < FZ_CIN * T; idx += 256) gx[idx] = R0[idx] + R1[idx];
+        return;
+    }
     const AdamArgs& Ad = A.adam;
     const float eps = A.scal[0];
     const int step = min(max(*A.step, 1), A.table_len);

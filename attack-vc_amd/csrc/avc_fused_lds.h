@@ -18,4 +18,13 @@ __host__ __device__ constexpr int fz_lds_bwd_main(int prec, int T) {
 }
 // + per-wave fold scratch [5*16 ch][8 edge columns] fp32
 __host__ __device__ constexpr int fz_lds_bwd(int prec, int T) { return fz_lds_bwd_main(prec, T) + 4 * 5 * 16 * 8 * 4; }
+
+// fused Decoder (avc_vc.hip) at output length Tn: forward = block-input image + conv1
+// output image, (Tn + 2P) rows each; backward = two dY images (Tn + 8 rows) + per-wave
+// fold scratch [2*16 ch][8 edge columns] fp32.  (+ 32 B static LDS in the forward)
+constexpr int DZ_FOLD_FLOATS = 2 * 16 * 8;
+__host__ __device__ constexpr int dz_lds_fwd(int prec, int Tn, int ks) { return 2 * (Tn + 2 * (ks / 2)) * fz_rs(prec); }
+__host__ __device__ constexpr int dz_lds_bwd(int prec, int Tn) {
+    return 2 * (Tn + 8) * fz_rs(prec) + 4 * DZ_FOLD_FLOATS * 4;
+}
 }  // namespace avc

@@ -137,6 +137,8 @@ struct FusedW {
     const float* b_in;
     const float* b_c1[FZ_MAXBLK];
     const float* b_c2[FZ_MAXBLK];
+    const void* mean_w;               // ContentEncoder mean_layer 1x1: M=128, K=128 (CE packs only)
+    const float* b_mean;
 };
 
 struct FusedArgs {
@@ -152,9 +154,72 @@ struct FusedArgs {
     int32_t* tick;                    // fwd: block 0 advances the Adam step counter
     const int32_t* step;              // bwd: Adam step (1-based)
     const float* scal;                // [0] = attack eps
-    int32_t table_len, pad_;
+    int32_t table_len;
+    int32_t ce_mode;                  // fwd: ContentEncoder (InstanceNorm before every act after the
+                                      // bank, mean_layer output to mu_out instead of the time-mean)
+    float* mu_out;                    // fwd, ce_mode: [B][128][T_N]
+    float* gx_out;                    // bwd: if set, write d loss / d x [B][80][T] here (no Adam)
     AdamArgs adam;                    // bwd: Adam update + next adv
     FusedW w;
+};
+
+// ---------------------------------------------------------------------------------
+// Fused per-utterance Decoder (avc_vc.hip, models.py:346-435) for the e2e / feedback
+// attacks.  Same layout rules as the SpeakerEncoder engine: wave w owns channels
+// [32w, 32w+32) of every 128-channel layer.  A x2 pixel-shuffle conv (128 -> 256
+// channels) runs as two half-GEMMs over its even (s = 0) and odd (s = 1) output
+// channels: half s of channel c is the frame 2t+s of the shuffled output.
+// ---------------------------------------------------------------------------------
+constexpr int DZ_MAXBLK = 8;
+constexpr int DZ_COUT = 80;
+
+struct DecW {
+    const void* in;                   // in_conv 1x1: M=128, K=128
+    const void* c1[DZ_MAXBLK];        // M=128, K=ks*128, K index (tap, channel)
+    const void* c2[DZ_MAXBLK][2];     // half s: rows 2c+s of second_conv (up=1: [0] only)
+    const void* out;                  // out_conv 1x1: M=80, K=128
+    const void* c1T[DZ_MAXBLK];       // dgrad: A[ci][(j, co)] = W1[co][ci][j]
+    const void* c2T[DZ_MAXBLK][2];    // dgrad of half s: A[ci][(j, c)] = W2[2c+s][ci][j]
+    const void* outT;                 // M=128, K=80: A[ci][co] = Wout[co][ci]
+    const float* b_in;
+    const float* b_c1[DZ_MAXBLK];
+    const float* b_c2[DZ_MAXBLK][2];  // bias of half s
+    const float* b_out;
+};
+
+struct DecArgs {
+    int32_t B, ks, nblk, act;
+    int32_t up[DZ_MAXBLK];
+    int32_t Tl[DZ_MAXBLK + 1];        // lengths: Tl[0] = content length, Tl[l+1] = Tl[l] * up[l]
+    int32_t stash_off[2 * DZ_MAXBLK]; // per InstanceNorm layer q = 2l (conv1), 2l+1 (conv2): float offset
+    int32_t stash_per_utt;            // floats per utterance (0: no stash, forward only)
+    const float* mu;                  // [B][128][Tl[0]] ContentEncoder mean
+    const float* cond;                // [B][2*nblk][256] conv_affine outputs (mean | std)
+    float* out;                       // [B][80][Tl[nblk]]
+    float* stash;                     // [B][stash_per_utt] normalised activations (fwd -> bwd)
+    float* invstd;                    // [B][2*nblk][128]
+    // e2e loss (fwd): MSE(out, tgt_out) - 0.1 MSE(out, org_out) and its gradient
+    const float* tgt_out;
+    const float* org_out;
+    float* g_out;                     // [B][80][Tl[nblk]]
+    float* losses;                    // [n_iters][B] or null
+    const int32_t* step;
+    const float* scal;                // [2] = 2 / n_elems of the output MSE
+    int32_t loss_len, pad_;
+    // bwd
+    const float* g_in;                // [B][80][Tl[nblk]] d loss / d out
+    float* g_cond;                    // [B][2*nblk][256]
+    DecW w;
+};
+
+// Batched dense layer over utterances: Y[b][m] = sum_k A[m][k] X[b][k] (+ bias[m])
+// (the decoder's conv_affine Linear layers and their transposes).
+struct DenseArgs {
+    const float* A;                   // [M][K] row-major
+    const float* X;                   // [B][K]
+    const float* bias;                // [M] or null
+    float* Y;                         // [B][M]
+    int32_t M, K, B, pad_;
 };
 
 }  // namespace avc

@@ -292,6 +292,8 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
 // (conflict-free, broadcast over the 16 rows of a wave).  Its 2 partial dot products
 // are summed over q with two xor-shuffles.  Weights are fetched four steps ahead (each
 // step otherwise waits a full MALL round trip).
+// Modes: 0 = forward (EMB -> emb_out); 1 = emb attack (loss vs tgt/org, backward ->
+// g_pooled); 3 = backward from a given d loss / d EMB (passed as `tgt`) -> g_pooled.
 // Step i (0 <= i < NL, nf = 2nd + 1 forward steps):
 //   i <  2nd : Y_i = act(W_i X + b_i), X = E (i even) / Y_{i-1} (i odd); E += Y_i (i odd)
 //   i == 2nd : EMB = W_out E + b_out;  loss and GA = d loss / d EMB
@@ -450,7 +452,9 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
             if (own) {
                 const f32x2 e = o + Bs[2 * nd * C + m];
                 EMB[m] = e;
-                if (mode != 0) {
+                if (mode == 3) {
+                    GA[m] = TG[m];   // d loss / d emb handed in (e2e / fb: through the decoder)
+                } else if (mode != 0) {
                     // loss = MSE(emb, tgt) - 0.1 MSE(emb, org) (attack_utils.py:81-82)
                     f32x2 g, q1, q2;
 #pragma unroll
@@ -474,7 +478,7 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
                 }
             }
             __syncthreads();
-            if (mode != 0 && tid < 64 * HV) {
+            if (mode == 1 && tid < 64 * HV) {
                 // per-utterance loss: wave u sums over d in a fixed order (stored at the end)
                 const int u = tid >> 6, lane = tid & 63;
                 float s1 = 0.f, s2 = 0.f;
@@ -538,7 +542,7 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     if (NL - nfull > 0) run_step(nfull, w0);
     if (NL - nfull > 1) run_step(nfull + 1, w1);
     if (NL - nfull > 2) run_step(nfull + 2, w2);
-    if (mode != 0 && losses && step_no >= 1 && step_no <= loss_len && tid < HV) {
+    if (mode == 1 && losses && step_no >= 1 && step_no <= loss_len && tid < HV) {
         const int b = u0 + tid;
         if (b < Bn) losses[(size_t)(step_no - 1) * Bn + b] = LS[tid];
     }

@@ -1,0 +1,689 @@
+// Fused per-utterance AdaIN-VC Decoder (models.py:346-435) for the e2e and feedback
+// attacks (attack_utils.py:7-48, 89-130) on gfx950, in the layout and GEMM machinery of
+// the SpeakerEncoder engine (avc_fused_core.h): one workgroup of 4 waves per utterance,
+// wave w owns channels [32w, 32w+32) of every 128-channel layer, every Conv1d and every
+// Conv1d input-gradient runs on MFMA out of LDS operand images.
+//
+// InstanceNorm1d (affine=False) is per (utterance, channel) over time, so it is
+// wave-local here: a channel's frames are the 16 lanes of a lane group times the
+// fragments of one register row (inorm_rows).  AdaIN (append_cond, models.py:66-79)
+// is y * std[c] + mean[c] with [mean | std] = conv_affine(emb), precomputed for the
+// batch by dense_batched.  A x2 pixel-shuffle conv (128 -> 256 channels, then
+// out[c][2t+s] = in[2c+s][t], models.py:33-49) runs as two half-GEMMs over the even /
+// odd output channels, so half s of channel c IS frame 2t+s of the shuffled output:
+// the shuffle, the nearest x2 upsample of the residual (models.py:52-63) and their
+// adjoints become lane-local adds plus one lane permutation of the residual stream.
+//
+//   dec_fwd_fused : mu (ContentEncoder mean) -> in_conv -> IN -> act -> 6 blocks
+//                   [conv1 -> IN -> AdaIN -> act -> conv2 (-> shuffle) -> IN -> AdaIN ->
+//                   act -> + (upsampled) residual] -> out_conv; stashes the normalised
+//                   activations (and 1/std) for the backward; e2e: MSE loss + gradient.
+//   dec_bwd_fused : d loss / d out -> out_conv^T -> blocks in reverse -> d loss /
+//                   d [mean | std] of every AdaIN (d loss / d emb follows through the
+//                   transposed conv_affine layers, dense_batched).  mu is constant in the
+//                   attacks, so the backward stops at the first AdaIN.
+#include "avc_fused_core.h"
+#include "avc_fused_lds.h"
+
+namespace avc {
+
+// the AdaIN-VC decoder at its config.yaml defaults on a 16-frame content code (T = 128)
+struct StdDec {
+    static constexpr int T0 = 16, NBLK = 6, KSZ = 5;
+    static constexpr int up(int l) { return (l & 1) ? 1 : 2; }
+    static constexpr int Tl(int l) {
+        int t = T0;
+        for (int i = 0; i < l; ++i) t *= up(i);
+        return t;
+    }
+    static constexpr int nf(int frames) { return (frames + 15) / 16; }
+};
+
+// stash slot of (half, fragment f, tile i) for this wave: 4 floats per lane, one 1 KiB
+// coalesced store per (half, f, i); nfq = fragments of the layer's frames
+__device__ __forceinline__ float* dz_stash(const DecArgs& A, int b, int q, int half, int nfq, int f, int i, int w) {
+    return A.stash + (size_t)b * A.stash_per_utt + A.stash_off[q] +
+           ((size_t)(((half * nfq + f) * 4 + w) * 2 + i) * 64 + (threadIdx.x & 63)) * 4;
+}
+
+// InstanceNorm over the two halves of a shuffled layer (2*T frames per channel)
+template <int NF>
+__device__ __forceinline__ void inorm_rows2(f32x4 (&v0)[2][NF], f32x4 (&v1)[2][NF], int nf, int T, f32x4 (&invstd)[2]) {
+    const int c = threadIdx.x & 15;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+            if (f < nf && 16 * f + c < T) s += v0[i][f] + v1[i][f];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o);
+        f32x4 mean;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mean[r] = s[r] / (float)(2 * T);
+        f32x4 q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+            if (f < nf && 16 * f + c < T) {
+                const f32x4 d0 = v0[i][f] - mean, d1 = v1[i][f] - mean;
+                q += d0 * d0 + d1 * d1;
+            }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) q[r] += __shfl_xor(q[r], o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) invstd[i][r] = 1.f / sqrtf(q[r] / (float)(2 * T) + 1e-5f);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            v0[i][f] = (v0[i][f] - mean) * invstd[i];
+            v1[i][f] = (v1[i][f] - mean) * invstd[i];
+        }
+    }
+}
+
+// sum over the frames of each owned channel row (16 lanes x fragments, t < T)
+template <int NF>
+__device__ __forceinline__ f32x4 row_sum(const f32x4 (&v)[NF], int nf, int T) {
+    const int c = threadIdx.x & 15;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+        if (f < nf && 16 * f + c < T) s += v[f];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o);
+    return s;
+}
+
+// zero rows [r0, r0+n) of this wave's 32-channel slice of an operand image
+template <int PREC>
+__device__ __forceinline__ void zero_rows(char* img, int r0, int n, int w) {
+    constexpr int RS = Fz<PREC>::RS;
+    constexpr int V16 = 32 * (int)sizeof(typename Fz<PREC>::E) / 16;
+    const int lane = threadIdx.x & 63;
+    for (int idx = lane; idx < n * V16; idx += 64) {
+        const int rr = idx / V16, part = idx - rr * V16;
+        *reinterpret_cast<f32x4*>(img + (r0 + rr) * RS + 32 * w * (int)sizeof(typename Fz<PREC>::E) + part * 16) =
+            f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------
+template <int PREC, int SH>
+__global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
+    using E = typename Fz<PREC>::E;
+    constexpr int RS = Fz<PREC>::RS;
+    constexpr int ESZ = (int)sizeof(E);
+    constexpr int VE = 16 / ESZ, KS = 4 * VE;
+    constexpr int NF = 8;
+    constexpr int STD = SH == 0 ? 1 : 0;
+    const int b = blockIdx.x;
+    const int nblk = STD ? StdDec::NBLK : A.nblk;
+    const int ks = STD ? StdDec::KSZ : A.ks;
+    const int P = ks / 2;
+    const int T0 = STD ? StdDec::T0 : A.Tl[0];
+    const int Tn = STD ? StdDec::Tl(StdDec::NBLK) : A.Tl[nblk];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, kq = lane >> 4;
+    const int ch0 = 32 * w + 4 * kq;
+    const int act = A.act;
+    const float* cond = A.cond + (size_t)b * (2 * nblk) * 256;
+    const bool stash = A.stash_per_utt > 0;
+
+    char* HB = fz_lds;                       // block input image [Tn + 2P] rows
+    char* YB = HB + (Tn + 2 * P) * RS;       // conv1 output image (first: the mu operand)
+
+    {   // mu [128][T0] -> YB rows t (operand of the 1x1 in_conv)
+        const float* mu = A.mu + (size_t)b * FZ_C * T0;
+        for (int idx = tid; idx < FZ_C * T0; idx += 256) {
+            const int ci = idx / T0, t = idx - ci * T0;
+            st1<PREC>(YB + t * RS + ci * ESZ, mu[idx]);
+        }
+    }
+    __syncthreads();
+
+    const int ns_c = ks * FZ_C / KS;
+    const int ns_1 = FZ_C / KS;
+    auto op_in = [&]() __attribute__((always_inline)) { return aop(A.w.in, 2 * w, 2, ns_1, ns_1); };
+    auto op_c1 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2 = [&](int l, int s) __attribute__((always_inline)) { return aop(A.w.c2[l][s], 2 * w, 2, ns_c, ns_c); };
+    // out_conv: 80 rows = 5 tiles; waves take tiles {0,1}, {2,3}, {3,4}, {3,4} (the
+    // duplicates are computed and dropped)
+    auto op_out = [&]() __attribute__((always_inline)) { return aop(A.w.out, w < 2 ? 2 * w : 3, 2, ns_1, ns_1); };
+    ARing<2> ring;
+    ring_fill(ring, op_in());
+    int rb[NF];
+
+    // AdaIN (append_cond) of IN layer q on the normalised rows: z = yhat * std + mean
+    auto adain_act = [&](f32x4 (&v)[2][NF], int q) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const f32x4 mn = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
+            const f32x4 sd = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[i][f][r] = act_f(v[i][f][r] * sd[r] + mn[r], act);
+        }
+    };
+    auto put_stash = [&](const f32x4 (&v)[2][NF], int q, int half, int nfq, const f32x4 (&is)[2])
+                         __attribute__((always_inline)) {
+        if (!stash) return;
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+            if (f < nfq)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) *reinterpret_cast<f32x4*>(dz_stash(A, b, q, half, nfq, f, i, w)) = v[i][f];
+        if (half == 0 && c == 0)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                *reinterpret_cast<f32x4*>(A.invstd + ((size_t)b * 2 * nblk + q) * 128 + ch0 + 16 * i) = is[i];
+    };
+
+    // in_conv -> IN -> act (models.py:415-418): the residual stream hres (fp32 registers)
+    f32x4 hres[2][NF];
+    {
+        zero_acc(hres);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, T0 - 1);
+        if constexpr (STD)
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(hres, IC<StdDec::nf(StdDec::T0)>{}, ring, op_in(), op_c1(0), YB, rb);
+        else
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(hres, IC<NF>{}, ring, op_in(), op_c1(0), YB, rb);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_in + ch0 + 16 * i);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) hres[i][f] += bi;
+        }
+        f32x4 is[2];
+        inorm_rows(hres, NF, T0, is);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hres[i][f][r] = act_f(hres[i][f][r], act);
+                const int t = 16 * f + c;
+                if (t < T0) put_reflect<PREC>(HB, t, T0, P, (ch0 + 16 * i) * ESZ, hres[i][f]);
+            }
+    }
+    __syncthreads();
+
+    // one block (models.py:419-433); nfi: fragments of its input frames
+    auto block = [&](auto nfi, int l, int Ti, int up) __attribute__((always_inline)) {
+        const int nfq = (Ti + 15) >> 4;
+        f32x4 acc[2][NF];
+        // conv1 -> IN -> AdaIN(2l) -> act -> YB
+        zero_acc(acc);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, Ti - 1);
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c1(l), op_c2(l, 0), HB, rb);
+        {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_c1[l] + ch0 + 16 * i);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) acc[i][f] += bi;
+            }
+            f32x4 is[2];
+            inorm_rows(acc, nfi, Ti, is);
+            put_stash(acc, 2 * l, 0, nfq, is);
+            adain_act(acc, 2 * l);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const int t = 16 * f + c;
+                    if (f < nfi && t < Ti) put_reflect<PREC>(YB, t, Ti, P, (ch0 + 16 * i) * ESZ, acc[i][f]);
+                }
+        }
+        __syncthreads();
+        const AOp nxt = l + 1 < nblk ? op_c1(l + 1) : op_out();
+        if (up == 1) {
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c2(l, 0), nxt, YB, rb);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_c2[l][0] + ch0 + 16 * i);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) acc[i][f] += bi;
+            }
+            f32x4 is[2];
+            inorm_rows(acc, nfi, Ti, is);
+            put_stash(acc, 2 * l + 1, 0, nfq, is);
+            adain_act(acc, 2 * l + 1);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    hres[i][f] += acc[i][f];
+                    const int t = 16 * f + c;
+                    if (f < nfi && t < Ti) put_reflect<PREC>(HB, t, Ti, P, (ch0 + 16 * i) * ESZ, hres[i][f]);
+                }
+        } else {
+            // x2 shuffle conv as two half-GEMMs: half s of channel c = frame 2t+s
+            f32x4 a1[2][NF];
+            zero_acc(acc);
+            zero_acc(a1);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c2(l, 0), op_c2(l, 1), YB, rb);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(a1, nfi, ring, op_c2(l, 1), nxt, YB, rb);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const f32x4 b0 = *reinterpret_cast<const f32x4*>(A.w.b_c2[l][0] + ch0 + 16 * i);
+                const f32x4 b1 = *reinterpret_cast<const f32x4*>(A.w.b_c2[l][1] + ch0 + 16 * i);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    acc[i][f] += b0;
+                    a1[i][f] += b1;
+                }
+            }
+            f32x4 is[2];
+            inorm_rows2(acc, a1, nfi, Ti, is);
+            put_stash(acc, 2 * l + 1, 0, nfq, is);
+            put_stash(a1, 2 * l + 1, 1, nfq, is);
+            adain_act(acc, 2 * l + 1);
+            adain_act(a1, 2 * l + 1);
+            // residual: y + upsample(h) -- frame 2t+s takes h[t] (lane-local per half)
+            const int To = 2 * Ti;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    acc[i][f] += hres[i][f];
+                    a1[i][f] += hres[i][f];
+                    const int t = 16 * f + c;
+                    if (f < nfi && t < Ti) {
+                        put_reflect<PREC>(HB, 2 * t, To, P, (ch0 + 16 * i) * ESZ, acc[i][f]);
+                        put_reflect<PREC>(HB, 2 * t + 1, To, P, (ch0 + 16 * i) * ESZ, a1[i][f]);
+                    }
+                }
+            // the residual stream in the doubled frame layout: frame 16f'+c' = 2t+s with
+            // t = 8f' + c'/2 in fragment f'/2, lane 8(f'&1) + c'/2 of half s = c'&1
+#pragma unroll
+            for (int f2 = 0; f2 < NF; ++f2) {
+                const int srcl = (lane & 48) | (8 * (f2 & 1) + (c >> 1));
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float v0 = __shfl(acc[i][f2 >> 1][r], srcl);
+                        const float v1 = __shfl(a1[i][f2 >> 1][r], srcl);
+                        hres[i][f2][r] = (c & 1) ? v1 : v0;
+                    }
+            }
+        }
+        __syncthreads();
+    };
+    if constexpr (STD != 0) {
+        static_for<0, StdDec::NBLK>([&](auto L) __attribute__((always_inline)) {
+            constexpr int l = decltype(L)::value;
+            block(IC<StdDec::nf(StdDec::Tl(l))>{}, l, StdDec::Tl(l), StdDec::up(l));
+        });
+    } else {
+        for (int l = 0; l < nblk; ++l) block(IC<NF>{}, l, A.Tl[l], A.up[l]);
+    }
+
+    // out_conv (1x1, 128 -> 80) over the Tn frames of HB (rows P + t)
+    f32x4 acc[2][NF];
+    zero_acc(acc);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) rb[f] = P + min(16 * f + c, Tn - 1);
+    if constexpr (STD)
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<StdDec::nf(StdDec::Tl(StdDec::NBLK))>{}, ring, op_out(), op_out(), HB, rb);
+    else
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_out(), op_out(), HB, rb);
+    const int tile0 = w < 2 ? 2 * w : 3;
+    const bool e2e = A.tgt_out != nullptr;
+    const size_t obase = (size_t)b * DZ_COUT * Tn;
+    const float gscale = e2e ? A.scal[2] : 0.f;
+    float q1 = 0.f, q2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int tile = tile0 + i;
+        const bool mine = w < 2 || (w == 2 && i == 1);
+        if (!mine) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = 16 * tile + 4 * kq + r;
+            const float bo = A.w.b_out[co];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = 16 * f + c;
+                if (t >= Tn) continue;
+                const float o = acc[i][f][r] + bo;
+                const size_t idx = obase + (size_t)co * Tn + t;
+                A.out[idx] = o;
+                if (e2e) {
+                    // MSE(out, tgt) - 0.1 MSE(out, org) (attack_utils.py:41-43) and its gradient
+                    const float d1 = o - A.tgt_out[idx], d2 = o - A.org_out[idx];
+                    A.g_out[idx] = gscale * d1 + gscale * d2 * -0.1f;
+                    q1 += d1 * d1;
+                    q2 += d2 * d2;
+                }
+            }
+        }
+    }
+    if (e2e && A.losses) {
+        // per-utterance loss: wave partial sums (fixed butterfly) then a fixed-order sum
+        __shared__ float lsum[4][2];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            q1 += __shfl_xor(q1, o);
+            q2 += __shfl_xor(q2, o);
+        }
+        if (lane == 0) {
+            lsum[w][0] = q1;
+            lsum[w][1] = q2;
+        }
+        __syncthreads();
+        const int step = *A.step;
+        if (tid == 0 && step >= 1 && step <= A.loss_len) {
+            const float n = (float)(DZ_COUT * Tn);
+            const float s1 = (lsum[0][0] + lsum[1][0]) + (lsum[2][0] + lsum[3][0]);
+            const float s2 = (lsum[0][1] + lsum[1][1]) + (lsum[2][1] + lsum[3][1]);
+            A.losses[(size_t)(step - 1) * A.B + b] = s1 / n - 0.1f * (s2 / n);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// backward: d loss / d out -> d loss / d cond
+// ---------------------------------------------------------------------------------
+template <int PREC, int SH>
+__global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
+    using E = typename Fz<PREC>::E;
+    constexpr int RS = Fz<PREC>::RS;
+    constexpr int ESZ = (int)sizeof(E);
+    constexpr int VE = 16 / ESZ, KS = 4 * VE;
+    constexpr int NF = FZ_MAXNF;
+    constexpr int ZP = 4;
+    constexpr int STD = SH == 0 ? 1 : 0;
+    const int b = blockIdx.x;
+    const int nblk = STD ? StdDec::NBLK : A.nblk;
+    const int ks = STD ? StdDec::KSZ : A.ks;
+    const int P = ks / 2;
+    const int Tn = STD ? StdDec::Tl(StdDec::NBLK) : A.Tl[nblk];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, kq = lane >> 4;
+    const int ch0 = 32 * w + 4 * kq;
+    const int act = A.act;
+    const float* cond = A.cond + (size_t)b * (2 * nblk) * 256;
+    float* gcond = A.g_cond + (size_t)b * (2 * nblk) * 256;
+
+    char* GB = fz_lds;                          // dY image (half 0) [Tn + 2ZP] rows
+    char* GB2 = GB + (Tn + 2 * ZP) * RS;        // dY image of half 1 / the out_conv^T operand
+    float* FSCR = reinterpret_cast<float*>(GB2 + (Tn + 2 * ZP) * RS) + w * DZ_FOLD_FLOATS;
+    const int n16 = (Tn + 2 * ZP) * RS / 16;
+
+    // both images zero: pad rows, stale frames and the K padding of out_conv^T (80 -> KS)
+    for (int i = tid; i < 2 * n16; i += 256) reinterpret_cast<f32x4*>(GB)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    {   // g_in [80][Tn] -> GB2 rows t
+        const float* g = A.g_in + (size_t)b * DZ_COUT * Tn;
+        for (int idx = tid; idx < DZ_COUT * Tn; idx += 256) {
+            const int co = idx / Tn, t = idx - co * Tn;
+            st1<PREC>(GB2 + t * RS + co * ESZ, g[idx]);
+        }
+    }
+    __syncthreads();
+
+    const int ns_c = ks * FZ_C / KS;
+    const int ns_o = (DZ_COUT + KS - 1) / KS;
+    auto op_outT = [&]() __attribute__((always_inline)) { return aop(A.w.outT, 2 * w, 2, ns_o, ns_o); };
+    auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2T = [&](int l, int s) __attribute__((always_inline)) { return aop(A.w.c2T[l][s], 2 * w, 2, ns_c, ns_c); };
+    ARing<2> ring;
+    ring_fill(ring, op_outT());
+    int rb[NF];
+
+    // g(h_N) = out_conv^T g_out
+    f32x4 gh[2][NF];
+    zero_acc(gh);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, Tn - 1);
+    if constexpr (STD)
+        fz_gemm<PREC, 2, NF, DZ_COUT, 1>(gh, IC<StdDec::nf(StdDec::Tl(StdDec::NBLK))>{}, ring, op_outT(),
+                                         op_c2T(nblk - 1, 0), GB2, rb);
+    else
+        fz_gemm<PREC, 2, NF, DZ_COUT, 1>(gh, IC<8>{}, ring, op_outT(), op_c2T(nblk - 1, 0), GB2, rb);
+    __syncthreads();
+    // GB2 becomes the half-1 dY image: clear the out_conv^T operand
+    for (int i = tid; i < n16; i += 256) reinterpret_cast<f32x4*>(GB2)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+
+    // act + AdaIN + InstanceNorm backward of IN layer q over H halves of T frames, in
+    // place on g0 (half 0) / g1 (half 1):  z = yhat*std + mean,  g_z = g * act'(z),
+    //   d/dmean = sum g_z,  d/dstd = sum g_z yhat          -> g_cond[q]
+    //   d/dx = invstd (g_y - mean(g_y) - yhat mean(g_y yhat)),  g_y = g_z std
+    //        = invstd std (g_z - (sum g_z)/n - yhat (sum g_z yhat)/n)     (n = H*T)
+    auto adain_in_bwd = [&](f32x4 (&g0)[2][NF], f32x4 (&g1)[2][NF], int H, int q, int T, int nfq)
+                            __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const f32x4 mn = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
+            const f32x4 sd = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
+            const f32x4 is = *reinterpret_cast<const f32x4*>(A.invstd + ((size_t)b * 2 * nblk + q) * 128 + ch0 + 16 * i);
+            f32x4 yh0[NF], yh1[NF];
+            f32x4 gm = {0.f, 0.f, 0.f, 0.f}, gs = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                if (f >= nfq) continue;
+                const bool in = 16 * f + c < T;
+                yh0[f] = *reinterpret_cast<const f32x4*>(dz_stash(A, b, q, 0, nfq, f, i, w));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float z = g0[i][f][r] * act_d(yh0[f][r] * sd[r] + mn[r], act);
+                    g0[i][f][r] = z;
+                    if (in) {
+                        gm[r] += z;
+                        gs[r] += z * yh0[f][r];
+                    }
+                }
+                if (H == 2) {
+                    yh1[f] = *reinterpret_cast<const f32x4*>(dz_stash(A, b, q, 1, nfq, f, i, w));
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float z = g1[i][f][r] * act_d(yh1[f][r] * sd[r] + mn[r], act);
+                        g1[i][f][r] = z;
+                        if (in) {
+                            gm[r] += z;
+                            gs[r] += z * yh1[f][r];
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    gm[r] += __shfl_xor(gm[r], o);
+                    gs[r] += __shfl_xor(gs[r], o);
+                }
+            if (c == 0) {
+                *reinterpret_cast<f32x4*>(gcond + q * 256 + ch0 + 16 * i) = gm;
+                *reinterpret_cast<f32x4*>(gcond + q * 256 + 128 + ch0 + 16 * i) = gs;
+            }
+            const float inv_n = 1.f / (float)(H * T);
+            f32x4 k1, k2, k3;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                k1[r] = is[r] * sd[r];
+                k2[r] = gm[r] * inv_n;
+                k3[r] = gs[r] * inv_n;
+            }
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                if (f >= nfq) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    g0[i][f][r] = k1[r] * (g0[i][f][r] - k2[r] - yh0[f][r] * k3[r]);
+                    if (H == 2) g1[i][f][r] = k1[r] * (g1[i][f][r] - k2[r] - yh1[f][r] * k3[r]);
+                }
+            }
+        }
+    };
+
+    // one block backward; gh holds g(h_{l+1}) over To = Ti * up frames on entry and
+    // g(h_l) over Ti frames on exit
+    auto block = [&](auto nfc, int l, int Ti, int up) __attribute__((always_inline)) {
+        const int nfq = (Ti + 15) >> 4;
+        f32x4 g0[2][NF], g1[2][NF];
+        if (up == 2) {
+            // halves: g_s[t] = g(h)[2t+s]: fragment 2f + (c >= 8), lane (2c+s) & 15
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                if (f >= nfq) continue;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int srcl = (lane & 48) | ((2 * c + s) & 15);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float va = __shfl(gh[i][2 * f < NF ? 2 * f : NF - 1][r], srcl);
+                            const float vb = __shfl(gh[i][2 * f + 1 < NF ? 2 * f + 1 : NF - 1][r], srcl);
+                            const float v = c < 8 ? va : vb;
+                            if (s == 0) g0[i][f][r] = v;
+                            else g1[i][f][r] = v;
+                        }
+                }
+            }
+            // the residual branch: adjoint of the x2 nearest upsample
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+                    if (f < nfq) gh[i][f] = g0[i][f] + g1[i][f];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+                    if (f < nfq) g0[i][f] = gh[i][f];
+        }
+        // conv2 branch: act, AdaIN(2l+1), IN backward -> dY images (half 0: GB, half 1: GB2)
+        adain_in_bwd(g0, g1, up, 2 * l + 1, Ti, nfq);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = 16 * f + c;
+                if (f < nfq && t < Ti) {
+                    st4<PREC>(GB + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, g0[i][f]);
+                    if (up == 2) st4<PREC>(GB2 + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, g1[i][f]);
+                }
+            }
+        zero_rows<PREC>(GB, ZP + Ti, ZP, w);      // frames past Ti (stale from longer layers)
+        if (up == 2) zero_rows<PREC>(GB2, ZP + Ti, ZP, w);
+        __syncthreads();
+        // conv2^T (both halves) over Ti interior frames + 2P pad positions, then the
+        // reflect-pad adjoint
+        const int ncol = Ti + 2 * P;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            const int n = 16 * f + c;
+            rb[f] = ZP + (n < ncol ? vpos(n, Ti, P) : 0) + P;
+        }
+        f32x4 acc[2][NF];
+        zero_acc(acc);
+        const AOp after = l > 0 ? op_c1T(l) : op_c2T(l, 0);
+        if (up == 2) {
+            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l, 0), op_c2T(l, 1), GB, rb);
+            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l, 1), after, GB2, rb);
+        } else {
+            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l, 0), after, GB, rb);
+        }
+        fold_edges(acc, Ti, P, FSCR);   // (barrier: GB / GB2 are free afterwards)
+        // conv1 branch: act, AdaIN(2l), IN backward; then conv1^T into the residual
+        // (the first block's conv1 input is the in_conv output: mu is constant, stop)
+        if (l > 0) {
+            adain_in_bwd(acc, g1, 1, 2 * l, Ti, nfq);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const int t = 16 * f + c;
+                    if (f < nfq && t < Ti) st4<PREC>(GB + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, acc[i][f]);
+                }
+            __syncthreads();
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c1T(l), op_c2T(l - 1, 0), GB, rb);
+            fold_edges(acc, Ti, P, FSCR);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+                    if (f < nfq) gh[i][f] += acc[i][f];
+        } else {
+            adain_in_bwd(acc, g1, 1, 0, Ti, nfq);   // g_cond[0] only
+        }
+    };
+    if constexpr (STD != 0) {
+        static_for<0, StdDec::NBLK>([&](auto L) __attribute__((always_inline)) {
+            constexpr int l = StdDec::NBLK - 1 - decltype(L)::value;
+            constexpr int Ti = StdDec::Tl(l);
+            block(IC<StdDec::nf(Ti + 2 * (StdDec::KSZ / 2))>{}, l, Ti, StdDec::up(l));
+        });
+    } else {
+        for (int l = nblk - 1; l >= 0; --l) block(IC<FZ_MAXNF>{}, l, A.Tl[l], A.up[l]);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// batched dense layer: Y[b][m] = sum_k A[m][k] X[b][k] (+ bias[m]); 64 rows x 16
+// utterances per workgroup, K in chunks of 32 staged through LDS
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) dense_batched(DenseArgs D) {
+    __shared__ float As[64][33];
+    __shared__ float Xs[16][33];
+    const int tid = threadIdx.x;
+    const int m0 = blockIdx.x * 64, b0 = blockIdx.y * 16;
+    const int ml = tid & 63, bg = tid >> 6;         // row, utterance group of 4
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < D.K; k0 += 32) {
+        for (int idx = tid; idx < 64 * 32; idx += 256) {
+            const int r = idx >> 5, kk = idx & 31;
+            As[r][kk] = (m0 + r < D.M && k0 + kk < D.K) ? D.A[(size_t)(m0 + r) * D.K + k0 + kk] : 0.f;
+        }
+        for (int idx = tid; idx < 16 * 32; idx += 256) {
+            const int u = idx >> 5, kk = idx & 31;
+            Xs[u][kk] = (b0 + u < D.B && k0 + kk < D.K) ? D.X[(size_t)(b0 + u) * D.K + k0 + kk] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int kk = 0; kk < 32; ++kk) {
+            const float a = As[ml][kk];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] = fmaf(a, Xs[4 * bg + u][kk], acc[u]);
+        }
+        __syncthreads();
+    }
+    const int m = m0 + ml;
+    if (m >= D.M) return;
+    const float bi = D.bias ? D.bias[m] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int bb = b0 + 4 * bg + u;
+        if (bb < D.B) D.Y[(size_t)bb * D.M + m] = acc[u] + bi;
+    }
+}
+
+#define AVC_DZ_INST(P, S)                                          \
+    template __global__ void dec_fwd_fused<P, S>(DecArgs);        \
+    template __global__ void dec_bwd_fused<P, S>(DecArgs);
+AVC_DZ_INST(PREC_F32, 0)
+AVC_DZ_INST(PREC_F32, 8)
+AVC_DZ_INST(PREC_BF16, 0)
+AVC_DZ_INST(PREC_BF16, 8)
+#undef AVC_DZ_INST
+
+}  // namespace avc

@@ -8,6 +8,10 @@
  *   avc_se_forward   replaces  SpeakerEncoder.forward    (/root/reference/models.py:327-343)
  *   avc_create       replaces  AdaInVC(config) + load_state_dict of the speaker encoder
  *                              (/root/reference/data_utils.py:219-221, models.py:213-283)
+ *   avc_e2e_attack   replaces  attack_utils.e2e_attack   (/root/reference/attack_utils.py:7-48)
+ *   avc_fb_attack    replaces  attack_utils.fb_attack    (/root/reference/attack_utils.py:89-130)
+ *   avc_inference    replaces  AdaInVC.inference         (/root/reference/models.py:472-489)
+ *   avc_attach_vc    replaces  load_state_dict of content_encoder / decoder (models.py:121-208, 346-435)
  *
  * The reference has no native code and no FFI of its own; the Python binding a
  * maintainer would add is shown in INTEGRATION.md (ctypes).
@@ -90,6 +94,49 @@ typedef struct avc_attack_opts {
 int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* ptb0,
                    int B, int T, float eps, int n_iters, float* out_adv,
                    const avc_attack_opts* opts, void* stream);
+
+/* ---- voice-conversion path: ContentEncoder + Decoder (e2e / feedback attacks) ----
+ * ContentEncoder / Decoder hyper-parameters, config.yaml model.ContentEncoder /
+ * model.Decoder (/root/reference/models.py:121-208, 346-435).  act: 0 = ReLU, 1 = LeakyReLU. */
+typedef struct avc_vc_cfg {
+    int32_t ce_c_in, ce_c_h, ce_c_out, ce_kernel_size;
+    int32_t ce_bank_size, ce_bank_scale, ce_c_bank, ce_n_conv_blocks;
+    int32_t ce_subsample[AVC_MAX_BLOCKS];
+    int32_t ce_act;
+    int32_t dec_c_in, dec_c_cond, dec_c_h, dec_c_out, dec_kernel_size, dec_n_conv_blocks;
+    int32_t dec_upsample[AVC_MAX_BLOCKS];
+    int32_t dec_act;
+} avc_vc_cfg;
+
+/* Number of fp32 values avc_attach_vc expects: content_encoder.* then decoder.* parameters,
+ * each in state_dict order (AdaInVC.state_dict() minus the speaker_encoder.* entries). */
+size_t avc_vc_weight_count(const avc_vc_cfg* cfg);
+
+/* Attach the ContentEncoder and Decoder of the same AdaInVC model to `ctx` (HOST weights).
+ * The HIP path is the fused per-utterance engine: the ContentEncoder must have the
+ * SpeakerEncoder engine's fused shape (c_in=80, c_h=c_bank=c_out=128, bank_scale=1,
+ * bank_size<=8, odd kernel_size<=5, <=8 blocks, subsample 1|2) and the Decoder c_in =
+ * c_cond = c_h = 128, c_out = 80, odd kernel_size <= 5, <= 8 blocks, upsample 1|2; the
+ * SpeakerEncoder of ctx must be fused-capable too.  Fails (non-zero) otherwise. */
+int avc_attach_vc(avc_ctx* ctx, const avc_vc_cfg* cfg, const float* weights, size_t n_weights);
+
+/* Frames of the Decoder output for T input frames (T -> ContentEncoder length -> x upsample). */
+int avc_vc_out_frames(avc_ctx* ctx, int T);
+
+/* out[B, 80, Tn] = AdaInVC.inference(src, tgt) = Decoder(ContentEncoder(src).mu,
+ * SpeakerEncoder(tgt))  (models.py:472-489); src, tgt [B, 80, T]; fp32. */
+int avc_inference(avc_ctx* ctx, const float* src, const float* tgt, int B, int T, float* out, void* stream);
+
+/* End-to-end attack (attack_utils.py:7-48) and feedback attack (attack_utils.py:89-130):
+ * same buffers and options as avc_emb_attack plus vc_src [B, c_in, T].  losses (optional)
+ * [n_iters, B]: e2e MSE(dec, tgt_out) - 0.1 MSE(dec, org_out); fb MSE(SE(dec), tgt_emb) -
+ * 0.1 MSE(SE(dec), org_emb), both before that step's update. */
+int avc_e2e_attack(avc_ctx* ctx, const float* vc_src, const float* vc_tgt, const float* adv_tgt,
+                   const float* ptb0, int B, int T, float eps, int n_iters, float* out_adv,
+                   const avc_attack_opts* opts, void* stream);
+int avc_fb_attack(avc_ctx* ctx, const float* vc_src, const float* vc_tgt, const float* adv_tgt,
+                  const float* ptb0, int B, int T, float eps, int n_iters, float* out_adv,
+                  const avc_attack_opts* opts, void* stream);
 
 /* Compute engine of a context.
  *  AUTO    (default): FUSED when the config and T allow it, else LAYERED.

@@ -1,0 +1,99 @@
+"""GPU parity of the voice-conversion path (ContentEncoder + Decoder, csrc/avc_vc.hip)
+through the C ABI: AdaInVC.inference and the e2e / feedback attacks against the
+reference's own outputs (tests/golden/full_T*.npz, made by the reference's
+attack_utils / models on CPU)."""
+import numpy as np
+import pytest
+import torch
+
+import attack_utils
+from helpers import TOL_GRAD_REL, check_adv, model_from_fixture, rel
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TOL_DEC_REL = 1e-4       # Decoder output relative to max |out| (six InstanceNorms deep, fp32)
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.fixture(scope="module")
+def full(golden):
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    z = golden("full_T128")
+    return z, model_from_fixture(z).to(DEV)
+
+
+@pytest.mark.parametrize("name", ["full_T128", "full_T127"])
+def test_inference_golden(full, golden, name):
+    """model.inference(vc_src, vc_tgt) (models.py:472-489) vs the reference's output;
+    T = 127 exercises the ceil-mode ContentEncoder and a 128-frame decoder output."""
+    z = golden(name)
+    _, m = full
+    out = m.inference(_dev(z["vc_src"]), _dev(z["vc_tgt"])).cpu().numpy()
+    assert out.shape == z["inference"].shape
+    assert rel(out, z["inference"]) <= TOL_DEC_REL, rel(out, z["inference"])
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_vc_attack_golden(full, kind):
+    """e2e_attack / fb_attack (attack_utils.py:7-48, 89-130) after 10 iterations, the
+    iteration-0 gradient and the per-iteration losses vs the reference's."""
+    z, m = full
+    fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
+    adv, info = fn(m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
+                   ptb0=_dev(z[f"{kind}_ptb0"]), return_info=True)
+    check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10)
+    assert rel(info["grad0"].cpu().numpy(), z[f"{kind}_grad0"]) <= 10 * TOL_GRAD_REL
+    np.testing.assert_allclose(info["losses"].cpu().numpy().T, z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_vc_attack_bf16_tracks_fp32(full, kind):
+    z, m = full
+    g = torch.Generator().manual_seed(5)
+    src, vc, at, p0 = (torch.randn(3, 80, 128, generator=g).to(DEV) for _ in range(4))
+    fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
+    a32, i32 = fn(m, src, vc, at, 0.1, 20, ptb0=p0, return_info=True)
+    a16, i16 = fn(m, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16", return_info=True)
+    a = i16["grad0"].cpu().numpy().reshape(3, -1).astype(np.float64)
+    b = i32["grad0"].cpu().numpy().reshape(3, -1).astype(np.float64)
+    cos = (a * b).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(b, axis=1)
+    assert cos.min() >= 0.99, cos
+    assert float((a16 - a32).abs().max()) <= 2e-2
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_vc_attack_deterministic_and_shard_invariant(full, kind):
+    z, m = full
+    g = torch.Generator().manual_seed(9)
+    src, vc, at, p0 = (torch.randn(10, 80, 128, generator=g).to(DEV) for _ in range(4))
+    fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
+    a = fn(m, src, vc, at, 0.1, 6, ptb0=p0).detach()
+    b = fn(m, src, vc, at, 0.1, 6, ptb0=p0).detach()
+    assert torch.equal(a, b)
+    lo = fn(m, src[:3], vc[:3], at[:3], 0.1, 6, ptb0=p0[:3]).detach()
+    hi = fn(m, src[3:], vc[3:], at[3:], 0.1, 6, ptb0=p0[3:]).detach()
+    assert torch.equal(torch.cat([lo, hi]), a)
+
+
+def test_vc_generic_length_runs(full):
+    """T = 100: ContentEncoder length 13, Decoder 13 -> 104 frames (generic kernel shapes)."""
+    z, m = full
+    g = torch.Generator().manual_seed(3)
+    src, vc, at, p0 = (torch.randn(2, 80, 100, generator=g).to(DEV) for _ in range(4))
+    out = m.inference(src, vc)
+    assert out.shape == (2, 80, 104) and torch.isfinite(out).all()
+    adv = attack_utils.e2e_attack(m, src, vc, at, 0.1, 3, ptb0=p0).detach()
+    assert torch.isfinite(adv).all() and float((adv - vc).abs().max()) <= 0.1 + 1e-6
+
+
+def test_vc_small_config_rejected(golden):
+    """c_h = 32 (tests/golden/small_T32.npz) is not the fused engine's shape: loud error,
+    no fallback."""
+    m = model_from_fixture(golden("small_T32")).to(DEV)
+    x = torch.zeros(1, 80, 32, device=DEV)
+    with pytest.raises(RuntimeError):
+        attack_utils.e2e_attack(m, x, x, x, 0.1, 1)
