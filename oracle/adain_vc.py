@@ -208,7 +208,7 @@ def se_backward(w, cfg, st, g_emb, p="speaker_encoder."):
 
 
 # ----------------------------------------------------------------------------------
-# ContentEncoder (models.py:121-210) and Decoder (models.py:346-435), forward only
+# ContentEncoder (models.py:121-210) forward, Decoder (models.py:346-435) forward + backward
 # ----------------------------------------------------------------------------------
 
 
@@ -243,22 +243,71 @@ def append_cond(x, cond):
     return x * cond[:, p:, None] + cond[:, :p, None]
 
 
-def dec_forward(w, cfg, z, cond, p="decoder."):
-    """Decoder.forward (models.py:403-435), sn=False."""
+def instance_norm_st(x, eps=1e-5):
+    """instance_norm that also returns (yhat, invstd) for the backward."""
+    mu = x.mean(axis=2, keepdims=True)
+    var = ((x - mu) ** 2).mean(axis=2, keepdims=True)
+    inv = 1 / np.sqrt(var + x.dtype.type(eps))
+    return (x - mu) * inv, inv
+
+
+def instance_norm_backward(g, yhat, inv):
+    """d/dx of (x - mean) * invstd (biased variance): invstd (g - mean(g) - yhat mean(g yhat))."""
+    return inv * (g - g.mean(axis=2, keepdims=True) - yhat * (g * yhat).mean(axis=2, keepdims=True))
+
+
+def dec_forward(w, cfg, z, cond, p="decoder.", st=None):
+    """Decoder.forward (models.py:403-435), sn=False.  st: optional list filled with
+    each block's (yhat1, z1, yhat2, z2, inv1, inv2, cond1, cond2) for dec_backward."""
     out = relu(instance_norm(pad_conv(z, w(p + "in_conv_layer.weight"), w(p + "in_conv_layer.bias"))))
     for l in range(cfg["n_conv_blocks"]):
         up = cfg["upsample"][l]
-        y = instance_norm(pad_conv(out, w(f"{p}first_conv_layers.{l}.weight"), w(f"{p}first_conv_layers.{l}.bias")))
-        y = relu(append_cond(y, linear(cond, w(f"{p}conv_affine_layers.{2*l}.weight"),
-                                       w(f"{p}conv_affine_layers.{2*l}.bias"))))
-        y = pad_conv(y, w(f"{p}second_conv_layers.{l}.weight"), w(f"{p}second_conv_layers.{l}.bias"))
+        c1 = linear(cond, w(f"{p}conv_affine_layers.{2*l}.weight"), w(f"{p}conv_affine_layers.{2*l}.bias"))
+        c2 = linear(cond, w(f"{p}conv_affine_layers.{2*l+1}.weight"), w(f"{p}conv_affine_layers.{2*l+1}.bias"))
+        yh1, inv1 = instance_norm_st(pad_conv(out, w(f"{p}first_conv_layers.{l}.weight"),
+                                              w(f"{p}first_conv_layers.{l}.bias")))
+        z1 = append_cond(yh1, c1)                                       # append_cond 66-79
+        y = pad_conv(relu(z1), w(f"{p}second_conv_layers.{l}.weight"), w(f"{p}second_conv_layers.{l}.bias"))
         if up > 1:
-            y = pixel_shuffle_1d(y, up)
-        y = instance_norm(y)
-        y = relu(append_cond(y, linear(cond, w(f"{p}conv_affine_layers.{2*l+1}.weight"),
-                                       w(f"{p}conv_affine_layers.{2*l+1}.bias"))))
-        out = y + (np.repeat(out, up, axis=2) if up > 1 else out)       # upsample 52-63 (nearest)
+            y = pixel_shuffle_1d(y, up)                                 # 33-49
+        yh2, inv2 = instance_norm_st(y)
+        z2 = append_cond(yh2, c2)
+        if st is not None:
+            st.append((yh1, z1, yh2, z2, inv1, inv2, c1, c2))
+        out = relu(z2) + (np.repeat(out, up, axis=2) if up > 1 else out)   # upsample 52-63 (nearest)
     return pad_conv(out, w(p + "out_conv_layer.weight"), w(p + "out_conv_layer.bias"))
+
+
+def _adain_backward(g, yhat, zpre, inv, cond):
+    """act + append_cond + InstanceNorm backward: returns (d/d conv output, d/d cond)."""
+    C = yhat.shape[1]
+    gz = g * (zpre > 0)
+    gcond = np.concatenate([gz.sum(axis=2), (gz * yhat).sum(axis=2)], axis=1)   # [mean | std]
+    return instance_norm_backward(gz * cond[:, C:, None], yhat, inv), gcond
+
+
+def dec_backward(w, cfg, st, g_out, p="decoder."):
+    """d loss / d cond of dec_forward given d loss / d out (the content code is constant
+    in the attacks, so the chain stops at the first block's AdaIN)."""
+    Wo = w(p + "out_conv_layer.weight")[:, :, 0]
+    gh = np.einsum("oc,bot->bct", Wo, g_out)
+    g_cond = np.zeros((g_out.shape[0], w(f"{p}conv_affine_layers.0.weight").shape[1]), dtype=g_out.dtype)
+    for l in reversed(range(cfg["n_conv_blocks"])):
+        up = cfg["upsample"][l]
+        yh1, z1, yh2, z2, inv1, inv2, c1, c2 = st[l]
+        B, C, To = gh.shape
+        T = To // up
+        g2, gc2 = _adain_backward(gh, yh2, z2, inv2, c2)
+        if up > 1:   # pixel_shuffle adjoint: pre[b, up*c + s, t] = post[b, c, up*t + s]
+            g2 = g2.reshape(B, C, T, up).transpose(0, 1, 3, 2).reshape(B, C * up, T)
+        ga1 = pad_conv_dgrad(g2, w(f"{p}second_conv_layers.{l}.weight"), 1, T)
+        g1, gc1 = _adain_backward(ga1, yh1, z1, inv1, c1)
+        g_cond += gc2 @ w(f"{p}conv_affine_layers.{2*l+1}.weight") + gc1 @ w(f"{p}conv_affine_layers.{2*l}.weight")
+        ghl = gh.reshape(B, C, T, up).sum(axis=3) if up > 1 else gh     # nearest-upsample adjoint
+        if l > 0:
+            ghl = ghl + pad_conv_dgrad(g1, w(f"{p}first_conv_layers.{l}.weight"), 1, T)
+        gh = ghl
+    return g_cond
 
 
 def inference(w, cfg, src, tgt):
@@ -314,33 +363,63 @@ class Adam:
 # ----------------------------------------------------------------------------------
 
 
-def emb_attack(w, cfg, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction="independent",
-               record=None):
-    """emb_attack (attack_utils.py:51-86) with an explicit ptb0.
+def attack(kind, w, cfg, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction="independent", record=None):
+    """emb / e2e / fb attack (attack_utils.py:51-86 / 7-48 / 89-130) with an explicit ptb0.
 
     reduction="independent": each utterance of the batch is its own attack
-    (loss summed over utterances, each an MSE mean over the embedding); equals
+    (loss summed over utterances, each an MSE mean over its own output); equals
     B separate reference calls.  reduction="mean": the loss is the reference's
-    MSE mean over the whole [B, D] batch, i.e. the reference called on the
-    batched tensor.  record: optional dict filled with "losses" and "grad0".
+    MSE mean over the whole batch, i.e. the reference called on the batched
+    tensor.  record: optional dict filled with "losses" and "grad0".
+    The ContentEncoder output of vc_src is computed once (it is constant).
     """
     se = cfg["SpeakerEncoder"] if "SpeakerEncoder" in cfg else cfg
     dt = vc_tgt.dtype.type
     ptb = ptb0.astype(vc_tgt.dtype).copy()
     opt = Adam(ptb)
-    org, _ = se_forward(w, se, vc_tgt)
-    tgt, _ = se_forward(w, se, adv_tgt)
-    B, D = org.shape
-    n_el = D if reduction == "independent" else B * D
+    if kind != "emb":
+        mu = ce_forward(w, cfg["ContentEncoder"], vc_src)
+        dec = cfg["Decoder"]
+
+        def infer(x, st_se=None, st_dec=None):
+            emb, st1 = se_forward(w, se, x)
+            if st_se is not None:
+                st_se.append(st1)
+            return dec_forward(w, dec, mu, emb, st=st_dec)
+    if kind == "emb":                                                  # attack_utils.py:73-75
+        org, _ = se_forward(w, se, vc_tgt)
+        tgt, _ = se_forward(w, se, adv_tgt)
+    elif kind == "e2e":                                                # 35-37
+        org, tgt = infer(vc_tgt), infer(adv_tgt)
+    else:                                                              # 117-119
+        org, _ = se_forward(w, se, infer(vc_tgt))
+        tgt, _ = se_forward(w, se, adv_tgt)
+    B = org.shape[0]
+    per = int(np.prod(org.shape[1:]))
+    n_el = per if reduction == "independent" else B * per
     losses = []
     for it in range(n_iters):
         th = np.tanh(ptb)
-        adv = vc_tgt + dt(eps) * th                                    # attack_utils.py:78
-        emb, st = se_forward(w, se, adv)
+        adv = vc_tgt + dt(eps) * th                                    # 78 / 40 / 122
+        if kind == "emb":
+            out, st = se_forward(w, se, adv)
+        else:
+            st_se, st_dec = [], []
+            out = infer(adv, st_se, st_dec)
+            if kind == "fb":
+                dec_out = out
+                out, st_fb = se_forward(w, se, dec_out)
+        flat = out.reshape(B, -1)
         if record is not None:
-            losses.append(emb_loss(emb, tgt, org, n_el))
-        g_emb = emb_loss_grad(emb, tgt, org, n_el)
-        g_adv = se_backward(w, se, st, g_emb)
+            losses.append(emb_loss(flat, tgt.reshape(B, -1), org.reshape(B, -1), n_el))
+        g = emb_loss_grad(out, tgt, org, n_el)
+        if kind == "emb":
+            g_adv = se_backward(w, se, st, g)
+        else:
+            if kind == "fb":
+                g = se_backward(w, se, st_fb, g)                       # d loss / d decoder output
+            g_emb = dec_backward(w, dec, st_dec, g)
+            g_adv = se_backward(w, se, st_se[0], g_emb)
         g = (g_adv * dt(eps)) * (dt(1) - th * th)                       # tanh backward
         if record is not None and it == 0:
             record["grad0"] = g.copy()
@@ -348,3 +427,18 @@ def emb_attack(w, cfg, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction="independe
     if record is not None:
         record["losses"] = np.stack(losses, axis=-1) if losses else None
     return vc_tgt + dt(eps) * np.tanh(ptb)
+
+
+def emb_attack(w, cfg, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction="independent", record=None):
+    """emb_attack (attack_utils.py:51-86) with an explicit ptb0 (see attack())."""
+    return attack("emb", w, cfg, None, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction, record)
+
+
+def e2e_attack(w, cfg, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction="independent", record=None):
+    """e2e_attack (attack_utils.py:7-48) with an explicit ptb0 (see attack())."""
+    return attack("e2e", w, cfg, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction, record)
+
+
+def fb_attack(w, cfg, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction="independent", record=None):
+    """fb_attack (attack_utils.py:89-130) with an explicit ptb0 (see attack())."""
+    return attack("fb", w, cfg, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, reduction, record)

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 import models
-from helpers import TOL_GRAD_REL, TOL_SE_REL, cfg_of, check_adv, model_from_fixture, oracle_weights, rel
+from helpers import TOL_GRAD_REL, TOL_GRAD_REL_FB, TOL_SE_REL, cfg_of, check_adv, model_from_fixture, oracle_weights, rel
 from oracle import adain_vc as oracle
 
 
@@ -113,3 +113,47 @@ def test_torch_cpu_baseline_is_reference_arithmetic(golden):
                                    torch.from_numpy(z["adv_tgt"][b:b + 1]), 0.1, 10,
                                    torch.from_numpy(z["emb_ptb0"][b:b + 1]))
         assert torch.equal(out, torch.from_numpy(z["emb_adv_n10"][b:b + 1]))
+
+
+@pytest.mark.parametrize("name", ["small_T32", "small_T33", "full_T128"])
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_vc_attacks(golden, name, kind):
+    """e2e / fb attacks (attack_utils.py:7-48, 89-130): numpy Decoder backward and the
+    attack loops vs the reference's 10-iteration outputs, grad0 and losses."""
+    z = golden(name)
+    if f"{kind}_adv_n10" not in z:
+        pytest.skip("fixture has no VC attack vectors")
+    w = oracle_weights(model_from_fixture(z))
+    rec = {}
+    adv = getattr(oracle, f"{kind}_attack")(w, cfg_of(z), z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 10,
+                                            z[f"{kind}_ptb0"], record=rec)
+    check_adv(adv, z[f"{kind}_adv_n10"], 10)
+    assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= (TOL_GRAD_REL_FB if kind == "fb" else TOL_GRAD_REL)
+    np.testing.assert_allclose(rec["losses"], z[f"{kind}_losses_n10"], rtol=1e-4, atol=1e-9)
+
+
+def test_decoder_backward_is_adjoint():
+    """<d out, J d cond> == <J^T d out, d cond> for the numpy Decoder (finite differences
+    in float64 on a tiny random decoder)."""
+    rng = np.random.default_rng(1)
+    C, cfg = 8, dict(n_conv_blocks=2, upsample=[2, 1])
+    sd = {"decoder.in_conv_layer.weight": rng.standard_normal((C, C, 1)), "decoder.in_conv_layer.bias": rng.standard_normal(C),
+          "decoder.out_conv_layer.weight": rng.standard_normal((5, C, 1)), "decoder.out_conv_layer.bias": rng.standard_normal(5)}
+    for l, up in enumerate(cfg["upsample"]):
+        sd[f"decoder.first_conv_layers.{l}.weight"] = rng.standard_normal((C, C, 5)) * 0.3
+        sd[f"decoder.first_conv_layers.{l}.bias"] = rng.standard_normal(C)
+        sd[f"decoder.second_conv_layers.{l}.weight"] = rng.standard_normal((C * up, C, 5)) * 0.3
+        sd[f"decoder.second_conv_layers.{l}.bias"] = rng.standard_normal(C * up)
+        for q in (2 * l, 2 * l + 1):
+            sd[f"decoder.conv_affine_layers.{q}.weight"] = rng.standard_normal((2 * C, 4)) * 0.5
+            sd[f"decoder.conv_affine_layers.{q}.bias"] = rng.standard_normal(2 * C)
+    w = oracle.Weights(sd, dtype=np.float64)
+    z, cond = rng.standard_normal((2, C, 7)), rng.standard_normal((2, 4))
+    st = []
+    out = oracle.dec_forward(w, cfg, z, cond, st=st)
+    g = rng.standard_normal(out.shape)
+    gc = oracle.dec_backward(w, cfg, st, g)
+    d = rng.standard_normal(cond.shape)
+    h = 1e-6
+    fd = ((oracle.dec_forward(w, cfg, z, cond + h * d) - oracle.dec_forward(w, cfg, z, cond - h * d)) * g).sum() / (2 * h)
+    assert abs(fd - (gc * d).sum()) <= 1e-6 * max(1.0, abs(fd))
