@@ -105,6 +105,7 @@ struct HeadArgs {
     float* g_pooled;          // fused path: [B][C] d loss / d pooled (replaces the g_hN expansion)
     const float* Wr;          // se_head_v: row-major dense [2nd][C][C], output [D][C]
     const float* WrT;         // se_head_v: their transposes [2nd][C][C], output^T [C][D]
+    int32_t tgt_parts;        // mode 3: d loss / d emb = sum of this many [B][D] slices at tgt
 };
 
 // ---------------------------------------------------------------------------------
@@ -214,12 +215,14 @@ struct DecArgs {
 
 // Batched dense layer over utterances: Y[b][m] = sum_k A[m][k] X[b][k] (+ bias[m])
 // (the decoder's conv_affine Linear layers and their transposes).
+// Split-K (gridDim.z = K / kchunk slices): slice z sums k in [z*kchunk, (z+1)*kchunk) into
+// Y + z*B*M; the consumer adds the slices in a fixed order (deterministic, no atomics).
 struct DenseArgs {
     const float* A;                   // [M][K] row-major
     const float* X;                   // [B][K]
-    const float* bias;                // [M] or null
-    float* Y;                         // [B][M]
-    int32_t M, K, B, pad_;
+    const float* bias;                // [M] or null (added by slice 0 only)
+    float* Y;                         // [gridDim.z][B][M]
+    int32_t M, K, B, kchunk;
 };
 
 }  // namespace avc

@@ -338,7 +338,19 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     const int tid = threadIdx.x, m = tid >> 2, q = tid & 3;
     const int u0 = blockIdx.x * HV;
     for (int idx = tid; idx < 2 * nd * C + D; idx += blockDim.x) Bs[idx] = A.bias[idx];
-    if (mode != 0)
+    if (mode == 3) {
+        // d loss / d emb: the split-K slices of the transposed conv_affine layers, summed
+        // in slice order (deterministic)
+        const int np = A.tgt_parts > 0 ? A.tgt_parts : 1;
+        for (int idx = tid; idx < D * HV; idx += blockDim.x) {
+            const int d = idx / HV, u = idx - d * HV;
+            const int b = u0 + u;
+            float g = 0.f;
+            if (b < Bn)
+                for (int q = 0; q < np; ++q) g += A.tgt[((size_t)q * Bn + b) * D + d];
+            reinterpret_cast<float*>(TG)[idx] = g;
+        }
+    } else if (mode != 0)
         for (int idx = tid; idx < D * HV; idx += blockDim.x) {
             const int d = idx / HV, u = idx - d * HV;
             const int b = u0 + u;

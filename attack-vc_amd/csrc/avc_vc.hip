@@ -640,23 +640,24 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
 
 // ---------------------------------------------------------------------------------
 // batched dense layer: Y[b][m] = sum_k A[m][k] X[b][k] (+ bias[m]); 64 rows x 16
-// utterances per workgroup, K in chunks of 32 staged through LDS
+// utterances per workgroup, K in chunks of 32 staged through LDS; blockIdx.z = K slice
 // ---------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) dense_batched(DenseArgs D) {
     __shared__ float As[64][33];
     __shared__ float Xs[16][33];
     const int tid = threadIdx.x;
     const int m0 = blockIdx.x * 64, b0 = blockIdx.y * 16;
+    const int kb = blockIdx.z * D.kchunk, ke = min(D.K, kb + D.kchunk);
     const int ml = tid & 63, bg = tid >> 6;         // row, utterance group of 4
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < D.K; k0 += 32) {
+    for (int k0 = kb; k0 < ke; k0 += 32) {
         for (int idx = tid; idx < 64 * 32; idx += 256) {
             const int r = idx >> 5, kk = idx & 31;
-            As[r][kk] = (m0 + r < D.M && k0 + kk < D.K) ? D.A[(size_t)(m0 + r) * D.K + k0 + kk] : 0.f;
+            As[r][kk] = (m0 + r < D.M && k0 + kk < ke) ? D.A[(size_t)(m0 + r) * D.K + k0 + kk] : 0.f;
         }
         for (int idx = tid; idx < 16 * 32; idx += 256) {
             const int u = idx >> 5, kk = idx & 31;
-            Xs[u][kk] = (b0 + u < D.B && k0 + kk < D.K) ? D.X[(size_t)(b0 + u) * D.K + k0 + kk] : 0.f;
+            Xs[u][kk] = (b0 + u < D.B && k0 + kk < ke) ? D.X[(size_t)(b0 + u) * D.K + k0 + kk] : 0.f;
         }
         __syncthreads();
 #pragma unroll 8
@@ -669,11 +670,12 @@ __global__ void __launch_bounds__(256) dense_batched(DenseArgs D) {
     }
     const int m = m0 + ml;
     if (m >= D.M) return;
-    const float bi = D.bias ? D.bias[m] : 0.f;
+    const float bi = (D.bias && blockIdx.z == 0) ? D.bias[m] : 0.f;
+    float* Y = D.Y + (size_t)blockIdx.z * D.B * D.M;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int bb = b0 + 4 * bg + u;
-        if (bb < D.B) D.Y[(size_t)bb * D.M + m] = acc[u] + bi;
+        if (bb < D.B) Y[(size_t)bb * D.M + m] = acc[u] + bi;
     }
 }
 

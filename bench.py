@@ -1,8 +1,10 @@
 """Benchmark: defended utterances/s of the AdaIN-VC embedding attack
 (n_iters=1500, eps=0.1) on MI355X — BASELINE.json `metric`, configs[1] workload
-(B=256 utterances of 80x128 normalized mel per GPU).
+(B=256 utterances of 80x128 normalized mel per GPU, bf16 MFMA operands with fp32
+accumulation / Adam state; the fp32 path is timed too and reported beside it).
+--attack e2e / fb measure configs[2] / [3] (end-to-end and feedback attacks).
 
-One "step" = one complete 1500-iteration emb attack over the rank's batch
+One "step" = one complete 1500-iteration attack over the rank's batch
 (inputs already resident in HBM).  N>1: one process per GPU (torchrun), each
 rank attacks its own contiguous shard of the global batch (no data-path
 collective; scaling "weak"), barrier + max-over-ranks timing.
@@ -40,8 +42,9 @@ FULL_CFG = {
     "Decoder": dict(c_in=128, c_cond=128, c_h=128, c_out=80, kernel_size=5, n_conv_blocks=6,
                     upsample=[2, 1, 2, 1, 2, 1], act="relu", sn=False, dropout_rate=0.0),
 }
-# emb FLOP per utterance-iteration (SpeakerEncoder fwd + input-grad)
-FLOP_PER_UTT_ITER = 518_848_512
+# FLOP per utterance-iteration (forward + input-gradient, ContentEncoder
+# hoisted out of the loop for e2e / fb)
+FLOP_PER_UTT_ITER = {"emb": 518_848_512, "e2e": 780_468_224, "fb": 1_299_316_736}
 PROF_ITERS = 10   # iterations of the HIP-event profiled pass (roofline)
 PEAK = {"fp32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}   # MI355X_MICROARCH.md
 
@@ -55,15 +58,17 @@ def parse():
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--n-iters", type=int, default=1500)
     ap.add_argument("--eps", type=float, default=0.1)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--attack", default="emb", choices=["emb", "e2e", "fb"])
+    ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
+    ap.add_argument("--no-fp32-compare", action="store_true", help="skip the fp32 comparison step")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(model, budget_s):
-    """Reference emb loop (torch CPU, B=1, all host threads used by ATen)."""
+def cpu_baseline(model, budget_s, kind="emb"):
+    """Reference attack loop (torch CPU, B=1, all host threads used by ATen)."""
     from oracle import torch_cpu
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
@@ -71,7 +76,14 @@ def cpu_baseline(model, budget_s):
     g = torch.Generator().manual_seed(1)
     vc, at = torch.randn(1, 80, 128, generator=g), torch.randn(1, 80, 128, generator=g)
     p0 = torch.randn(1, 80, 128, generator=torch.Generator().manual_seed(123))
-    torch_cpu.emb_attack(sd, FULL_CFG, vc, at, 0.1, 3, p0)            # warm-up
+    src = torch.randn(1, 80, 128, generator=g)
+
+    def run(n, hook=None):
+        if kind == "emb":
+            return torch_cpu.emb_attack(sd, FULL_CFG, vc, at, 0.1, n, p0, iter_hook=hook)
+        return torch_cpu.vc_attack(kind, sd, FULL_CFG, src, vc, at, 0.1, n, p0, iter_hook=hook)
+
+    run(3)                                                              # warm-up
     stamps = []
     t0 = time.perf_counter()
 
@@ -81,13 +93,13 @@ def cpu_baseline(model, budget_s):
             raise StopIteration
 
     try:
-        torch_cpu.emb_attack(sd, FULL_CFG, vc, at, 0.1, 1500, p0, iter_hook=hook)
+        run(1500, hook)
     except StopIteration:
         pass
     n = len(stamps)
     per_iter = (stamps[-1] - t0) / n
     return {"value": 1.0 / (per_iter * 1500), "unit": "utts/s", "cores": threads, "kind": "port",
-            "sample": f"B=1 emb_attack 80x128, {n} of 1500 iterations timed ({per_iter*1e3:.2f} ms/iter), "
+            "sample": f"B=1 {kind}_attack 80x128, {n} of 1500 iterations timed ({per_iter*1e3:.2f} ms/iter), "
                       f"scaled x1500; oracle/torch_cpu.py (reference ATen arithmetic incl. weight grads)"}
 
 
@@ -120,11 +132,15 @@ def main():
     at_all = torch.randn(total, 80, T, generator=g)
     p0_all = torch.randn(total, 80, T, generator=torch.Generator().manual_seed(123))
     sl = shard.shard_slice(total, rank, world)
-    vc, at, p0 = (t[sl].contiguous().to(dev) for t in (vc_all, at_all, p0_all))
-    del vc_all, at_all, p0_all
+    src_all = torch.randn(total, 80, T, generator=g)
+    vc, at, p0, src = (t[sl].contiguous().to(dev) for t in (vc_all, at_all, p0_all, src_all))
+    del vc_all, at_all, p0_all, src_all
 
-    def step():
-        return attack_utils.emb_attack(model_dev, vc, at, a.eps, a.n_iters, ptb0=p0, precision=a.precision)
+    def step(prec=a.precision):
+        if a.attack == "emb":
+            return attack_utils.emb_attack(model_dev, vc, at, a.eps, a.n_iters, ptb0=p0, precision=prec)
+        fn = attack_utils.e2e_attack if a.attack == "e2e" else attack_utils.fb_attack
+        return fn(model_dev, src, vc, at, a.eps, a.n_iters, ptb0=p0, precision=prec)
 
     for _ in range(a.warmup):
         step()
@@ -142,11 +158,33 @@ def main():
     elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
     assert torch.isfinite(out).all()
 
+    fp32_cmp = None
+    if a.precision != "fp32" and not a.no_fp32_compare:
+        # the exact-fp32 path on the same workload (one untimed warm-up, one timed step)
+        step("fp32")
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        out32 = step("fp32")
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        e32 = shard.max_over_ranks(time.perf_counter() - t1, dist, dev)
+        fp32_cmp = {"value": round(total / e32, 3), "ms_per_step": round(e32 * 1e3, 3),
+                    "max_abs_diff_vs_bf16": float((out32 - out).detach().abs().max())}
+
     roof = None
     if not a.no_roofline:
-        ctx = avc_native.context_for(model_dev.speaker_encoder, dev)
+        if a.attack == "emb":
+            ctx = avc_native.context_for(model_dev.speaker_encoder, dev)
+        else:
+            ctx = avc_native.vc_context_for(model_dev, dev)
         ctx.set_profiling(True)
-        ctx.emb_attack(vc, at, p0, a.eps, PROF_ITERS, precision=a.precision)
+        if a.attack == "emb":
+            ctx.emb_attack(vc, at, p0, a.eps, PROF_ITERS, precision=a.precision)
+        else:
+            ctx.vc_attack(a.attack, src, vc, at, p0, a.eps, PROF_ITERS, precision=a.precision)
         ms_iter, stats = ctx.profile()
         ctx.set_profiling(False)
         name, (n, tot_ms, tot_fl) = max(stats.items(), key=lambda kv: kv[1][1])
@@ -167,23 +205,27 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(model, a.cpu_seconds)
+        cpu = cpu_baseline(model, a.cpu_seconds, a.attack)
 
     if rank == 0:
         ms = elapsed / a.steps * 1e3
         value = total * a.steps / elapsed
         base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+        metric = base["metric"] if a.attack == "emb" else \
+            f"defended utts/sec @ n_iters={a.n_iters} eps={a.eps} {a.attack}-attack; 1/2/4/8 MI355X"
+        cfg_no = {"emb": 1, "e2e": 2, "fb": 3}[a.attack]
+        fl = FLOP_PER_UTT_ITER[a.attack]
         line = {
-            "metric": base["metric"], "value": round(value, 3), "unit": "utts/s", "n_gpus": world,
+            "metric": metric, "value": round(value, 3), "unit": "utts/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
-            "config": {"workload": f"emb_attack B={B}/GPU T={T} n_iters={a.n_iters} eps={a.eps} "
-                                   f"(BASELINE configs[1]; AdaIN-VC SpeakerEncoder, random init seed 0)",
+            "config": {"workload": f"{a.attack}_attack B={B}/GPU T={T} n_iters={a.n_iters} eps={a.eps} "
+                                   f"(BASELINE configs[{cfg_no}]; AdaIN-VC, random init seed 0)",
                        "batch_per_gpu": B, "frames": T, "n_iters": a.n_iters, "eps": a.eps,
                        "parallelism": f"dp{world} (independent utterance shards, no collective)"},
-            "roofline": roof, "cpu_baseline": cpu,
-            "flop_per_utt_iter": FLOP_PER_UTT_ITER,
-            "tflops_whole_step": round(FLOP_PER_UTT_ITER * a.n_iters * total * a.steps / elapsed / 1e12, 2),
+            "roofline": roof, "cpu_baseline": cpu, "fp32": fp32_cmp,
+            "flop_per_utt_iter": fl,
+            "tflops_whole_step": round(fl * a.n_iters * total * a.steps / elapsed / 1e12, 2),
         }
         print(json.dumps(line), flush=True)
     if dist:

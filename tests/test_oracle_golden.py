@@ -157,3 +157,14 @@ def test_decoder_backward_is_adjoint():
     h = 1e-6
     fd = ((oracle.dec_forward(w, cfg, z, cond + h * d) - oracle.dec_forward(w, cfg, z, cond - h * d)) * g).sum() / (2 * h)
     assert abs(fd - (gc * d).sum()) <= 1e-6 * max(1.0, abs(fd))
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_torch_cpu_vc_baseline_matches_reference(golden, kind):
+    """bench.py's e2e / fb CPU baseline (oracle/torch_cpu.vc_attack) vs the reference's outputs."""
+    from oracle import torch_cpu
+    z = golden("small_T32")
+    sd = model_from_fixture(z).state_dict()
+    out = torch_cpu.vc_attack(kind, sd, cfg_of(z), torch.from_numpy(z["vc_src"][:1]), torch.from_numpy(z["vc_tgt"][:1]),
+                              torch.from_numpy(z["adv_tgt"][:1]), 0.1, 10, torch.from_numpy(z[f"{kind}_ptb0"][:1]))
+    check_adv(out.numpy(), z[f"{kind}_adv_n10"][:1], 10)
