@@ -1,10 +1,10 @@
 // avc_bench: native driver of libavc for rocprofv3 runs (no Python in the
-// profiled process).  Same workload as bench.py: full AdaIN-VC SpeakerEncoder
-// config, B utterances x 80 x T frames, n_iters Adam steps, eps 0.1.
+// profiled process).  Same workload as bench.py: full AdaIN-VC config, B utterances
+// x 80 x T frames, n_iters Adam steps, eps 0.1; attack 0 = emb, 1 = e2e, 2 = fb.
 // Weights/inputs are synthetic (uniform / normal from a fixed-seed generator):
 // kernel durations do not depend on the values.
 //
-//   avc_bench [B=256] [T=128] [n_iters=1500] [steps=1] [warmup=0] [precision 0=fp32 1=bf16]
+//   avc_bench [B=256] [T=128] [n_iters=1500] [steps=1] [warmup=0] [precision 0=fp32 1=bf16] [attack 0|1|2]
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -39,6 +39,7 @@ int main(int argc, char** argv) {
     const int steps = argc > 4 ? atoi(argv[4]) : 1;
     const int warmup = argc > 5 ? atoi(argv[5]) : 0;
     const int prec = argc > 6 ? atoi(argv[6]) : AVC_PREC_FP32;
+    const int attack = argc > 7 ? atoi(argv[7]) : 0;
 
     avc_se_cfg cfg{};
     cfg.c_in = 80;
@@ -61,12 +62,32 @@ int main(int argc, char** argv) {
     for (auto& v : w) v = uw(rng);
     avc_ctx* ctx = nullptr;
     CK(avc_create(0, &cfg, w.data(), nw, &ctx));
+    if (attack) {   // ContentEncoder + Decoder at the config.yaml defaults
+        avc_vc_cfg v{};
+        v.ce_c_in = 80;
+        v.ce_c_h = v.ce_c_out = v.ce_c_bank = 128;
+        v.ce_kernel_size = 5;
+        v.ce_bank_size = 8;
+        v.ce_bank_scale = 1;
+        v.ce_n_conv_blocks = 6;
+        for (int i = 0; i < 6; ++i) v.ce_subsample[i] = sub[i];
+        v.dec_c_in = v.dec_c_cond = v.dec_c_h = 128;
+        v.dec_c_out = 80;
+        v.dec_kernel_size = 5;
+        v.dec_n_conv_blocks = 6;
+        for (int i = 0; i < 6; ++i) v.dec_upsample[i] = (i & 1) ? 1 : 2;
+        std::vector<float> wv(avc_vc_weight_count(&v));
+        for (auto& x : wv) x = uw(rng);
+        CK(avc_attach_vc(ctx, &v, wv.data(), wv.size()));
+    }
 
     const size_t X = (size_t)B * cfg.c_in * T;
     std::normal_distribution<float> nd(0.f, 1.f);
-    std::vector<float> h(3 * X);
+    std::vector<float> h(4 * X);
     for (auto& v : h) v = nd(rng);
-    float *vc, *at, *p0, *out;
+    float *vc, *at, *p0, *out, *src;
+    HK(hipMalloc(&src, X * 4));
+    HK(hipMemcpy(src, h.data() + 3 * X, X * 4, hipMemcpyHostToDevice));
     HK(hipMalloc(&vc, X * 4));
     HK(hipMalloc(&at, X * 4));
     HK(hipMalloc(&p0, X * 4));
@@ -78,10 +99,15 @@ int main(int argc, char** argv) {
     avc_attack_opts o{};
     o.use_graph = 1;
     o.precision = prec;
-    for (int i = 0; i < warmup; ++i) CK(avc_emb_attack(ctx, vc, at, p0, B, T, 0.1f, n_iters, out, &o, nullptr));
+    auto run = [&](int n) {
+        if (attack == 1) return avc_e2e_attack(ctx, src, vc, at, p0, B, T, 0.1f, n, out, &o, nullptr);
+        if (attack == 2) return avc_fb_attack(ctx, src, vc, at, p0, B, T, 0.1f, n, out, &o, nullptr);
+        return avc_emb_attack(ctx, vc, at, p0, B, T, 0.1f, n, out, &o, nullptr);
+    };
+    for (int i = 0; i < warmup; ++i) CK(run(n_iters));
     HK(hipDeviceSynchronize());
     auto t0 = std::chrono::steady_clock::now();
-    for (int i = 0; i < steps; ++i) CK(avc_emb_attack(ctx, vc, at, p0, B, T, 0.1f, n_iters, out, &o, nullptr));
+    for (int i = 0; i < steps; ++i) CK(run(n_iters));
     HK(hipDeviceSynchronize());
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::vector<float> res(X);
@@ -93,7 +119,7 @@ int main(int argc, char** argv) {
            B, T, n_iters, steps, s, B * steps / s, s * 1e3 / (steps * (double)n_iters), cs);
     // per-kernel HIP-event profile of 3 iterations
     CK(avc_set_profiling(ctx, 1));
-    CK(avc_emb_attack(ctx, vc, at, p0, B, T, 0.1f, 3, out, &o, nullptr));
+    CK(run(3));
     HK(hipDeviceSynchronize());
     double ms_it = 0, fl_it = 0;
     CK(avc_get_profile(ctx, &ms_it, &fl_it));

@@ -199,7 +199,8 @@ def main():
                                    "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 2)} for k, v in stats.items()}}
         tpath = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tpath):
-            tr = json.load(open(tpath)).get(name)
+            key = a.attack + ("_fp32" if a.precision == "fp32" else "")
+            tr = json.load(open(tpath)).get(key, {}).get(name)
             if tr is not None:
                 roof["traffic"] = tr
 

@@ -5,8 +5,9 @@ fused-engine emb attack, native driver) into profiles/:
   <round>_fused_<prec>_summary.md          per kernel: median duration, algorithmic
                                            TFLOP/s, HBM bytes and GB/s, MFMA busy,
                                            wave wait/active split, LDS conflicts, L2 hit
-  traffic.json                             HBM bytes per launch per kernel name, in the
-                                           names bench.py's roofline uses
+  traffic.json                             HBM bytes per launch per kernel name, keyed by
+                                           workload ("emb", "e2e", "fb", "emb_fp32"), in the
+                                           kernel names bench.py's roofline uses
 
 HBM bytes per dispatch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
 FETCH_SIZE counts half the bytes of 16-B-per-lane streaming reads
@@ -24,14 +25,19 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # algorithmic FLOP per launch at B=256, T=128 (259,424,256 per utterance
 # per direction); the head's dense chain is not counted as conv work
-FLOP = {"se_fwd_fused": 259_424_256 * 256, "se_bwd_fused": 259_424_256 * 256}
+FLOP = {"se_fwd_fused": 259_424_256 * 256, "se_bwd_fused": 259_424_256 * 256,
+        # Decoder conv MACs x 2 (avc_vc_host.inc dec_mac): forward 65,798,144, backward 64,225,280
+        # MAC per utterance at T0 = 16
+        "dec_fwd_fused": 2 * 65_798_144 * 256, "dec_bwd_fused": 2 * 64_225_280 * 256,
+        "dense_batched": 2 * 3072 * 128 * 256}
+ATTACK = {0: "emb", 1: "e2e", 2: "fb"}
 
 
 def short(k):
-    m = re.search(r"(se_fwd_fused|se_bwd_fused)<(\d), (\d)>", k)
+    m = re.search(r"(se_fwd_fused|se_bwd_fused|dec_fwd_fused|dec_bwd_fused)<(\d), (\d)>", k)
     if m:
         return "%s<%s>" % (m.group(1), "f32" if m.group(2) == "0" else "bf16")
-    for n in ("se_head_v", "se_head", "attack_init"):
+    for n in ("se_head_v", "se_head", "attack_init", "dense_batched"):
         if n in k:
             return n
     return k.split("(")[0][:60]
@@ -41,11 +47,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dir", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--prec", type=int, default=1)
+    ap.add_argument("--attack", type=int, default=0)
     ap.add_argument("--round", default="r01")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles"))
     a = ap.parse_args()
-    pname = "fp32" if a.prec == 0 else "bf16"
-    base = os.path.join(a.dir, f"fz_p{a.prec}")
+    pname = ("fp32" if a.prec == 0 else "bf16") + ("" if a.attack == 0 else "_" + ATTACK[a.attack])
+    base = os.path.join(a.dir, f"fz_p{a.prec}_a{a.attack}")
     os.makedirs(a.out, exist_ok=True)
     shutil.copy(os.path.join(base, "trace", "run_kernel_stats.csv"),
                 os.path.join(a.out, f"{a.round}_fused_{pname}_kernel_stats.csv"))
@@ -72,9 +79,10 @@ def main():
         return statistics.mean(v) if v else None
 
     f = lambda x, fmt: (fmt % x) if x is not None else "-"
-    md = [f"# rocprofv3 summary {a.round}: fused engine, {pname} emb attack (B=256, T=128)", "",
-          f"Source: `PREC={a.prec} scripts/pmc_fused.sh` on one MI355X: native driver "
-          f"`attack-vc_amd/avc_bench 256 128 <iters> 1 0 {a.prec}` (default engine = fused), "
+    md = [f"# rocprofv3 summary {a.round}: fused engine, {pname.split('_')[0]} {ATTACK[a.attack]} attack "
+          f"(B=256, T=128)", "",
+          f"Source: `PREC={a.prec} ATTACK={a.attack} scripts/pmc_fused.sh` on one MI355X: native driver "
+          f"`attack-vc_amd/avc_bench 256 128 <iters> 1 0 {a.prec} {a.attack}` (default engine = fused), "
           "one `--kernel-trace --stats` run plus one run per PMC pass.", "",
           "| kernel | launches | median us | TFLOP/s (alg.) | HBM MB/launch | HBM GB/s | MFMA busy | "
           "wait/wave | active/wave | LDS confl/LDS cyc | L2 hit |",
@@ -105,7 +113,10 @@ def main():
     open(os.path.join(a.out, f"{a.round}_fused_{pname}_summary.md"), "w").write("\n".join(md) + "\n")
     tpath = os.path.join(a.out, "traffic.json")
     allt = json.load(open(tpath)) if os.path.exists(tpath) else {}
-    allt.update(traffic)
+    if not all(isinstance(v, dict) for v in allt.values()):
+        allt = {}                                  # (old flat layout)
+    key = ATTACK[a.attack] + ("_fp32" if a.prec == 0 else "")
+    allt[key] = traffic
     json.dump(allt, open(tpath, "w"), indent=1, sort_keys=True)
     print("\n".join(md))
 
