@@ -564,6 +564,25 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
                 Wr[2 * nd * CC + (size_t)r * c.c_h + perm(k, c.c_h)] = oW[(size_t)r * c.c_h + k];
                 WrT[2 * nd * CC + (size_t)k * c.c_out + perm(r, c.c_out)] = oW[(size_t)r * c.c_h + k];
             }
+        // lane-interleave for coalesced loads: thread t = 4m + q of se_head_v (wave t/64,
+        // lane t%64) reads its 32 permuted weights as 8 f32x4 chunks; chunk e of every lane
+        // of a wave is stored contiguously, so each of the 8 load instructions reads one
+        // 1 KiB run instead of 16 B from each of 64 different lines
+        auto interleave = [&](std::vector<float>& W) {
+            if (c.c_h != 128 || c.c_out != 128) return;   // se_head_v's shape (fused engine)
+            std::vector<float> o(W.size());
+            for (size_t mat = 0; mat < W.size() / (128 * 128); ++mat) {
+                const float* src = W.data() + mat * 128 * 128;
+                float* dst = o.data() + mat * 128 * 128;
+                for (int t = 0; t < 512; ++t)
+                    for (int e = 0; e < 8; ++e)
+                        for (int j = 0; j < 4; ++j)
+                            dst[((size_t)((t / 64) * 8 + e) * 64 + (t % 64)) * 4 + j] = src[(size_t)t * 32 + 4 * e + j];
+            }
+            W.swap(o);
+        };
+        interleave(Wr);
+        interleave(WrT);
         up(ctx->head_Wr, Wr);
         up(ctx->head_WrT, WrT);
     }

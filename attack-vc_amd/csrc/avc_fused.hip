@@ -85,6 +85,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
     const int act = A.act;
+    FZ_PH_DECL
+    FZ_PH();
     if (A.tick && b == 0 && tid == 0) atomicAdd(A.tick, 1);
 
     char* XB = fz_lds;                                  // x image [T+8][80], pad 4
@@ -99,18 +101,35 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     const int ch0 = 32 * w + 4 * kq;                    // + 16*i + r
     constexpr int WPL = FZ_MASK_WORDS_PER_LAYER / 4;    // mask words per (layer, wave)
 
-    // ---- x -> XB (transposed, reflect rows)
+    // ---- x -> XB (transposed, reflect rows).  16-byte loads, all of a thread's issued
+    // before any store (one HBM round trip, not one per element); 80*T is a multiple of 4
     {
-        const float* x = A.x + (size_t)b * FZ_CIN * T;
-        for (int idx = tid; idx < FZ_CIN * T; idx += 256) {
-            const int ci = idx / T, t = idx - ci * T;
-            const float v = x[idx];
-            st1<PREC>(XB + (4 + t) * RS + ci * ESZ, v);
-            if (t >= 1 && t <= 4) st1<PREC>(XB + (4 - t) * RS + ci * ESZ, v);
-            if (t >= T - 5 && t <= T - 2) st1<PREC>(XB + (4 + 2 * T - 2 - t) * RS + ci * ESZ, v);
+        const f32x4* x4 = reinterpret_cast<const f32x4*>(A.x + (size_t)b * FZ_CIN * T);
+        const int n4 = FZ_CIN * T / 4;
+        constexpr int XV = (FZ_CIN * 128 / 4 + 255) / 256;   // f32x4 per thread at T <= 128
+        f32x4 xv[XV];
+#pragma unroll
+        for (int k = 0; k < XV; ++k) {
+            const int q = tid + 256 * k;
+            xv[k] = q < n4 ? x4[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int k = 0; k < XV; ++k) {
+            const int q = tid + 256 * k;
+            if (q >= n4) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int idx = 4 * q + e;
+                const int ci = idx / T, t = idx - ci * T;
+                const float v = xv[k][e];
+                st1<PREC>(XB + (4 + t) * RS + ci * ESZ, v);
+                if (t >= 1 && t <= 4) st1<PREC>(XB + (4 - t) * RS + ci * ESZ, v);
+                if (t >= T - 5 && t <= T - 2) st1<PREC>(XB + (4 + 2 * T - 2 - t) * RS + ci * ESZ, v);
+            }
         }
     }
     __syncthreads();
+    FZ_PH();
 
     const auto nf0 = IC<G>{};
     const int ns_c = ks * FZ_C / KS;
@@ -141,6 +160,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, T - 1) + 4 - pl;
         fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc, nf0, ring, op_bank(kb), op_inb(kb), XB, rb);
+        FZ_PH();
         char* BK = (kb & 1) ? BK1 : BK0;
         const float* bias = A.w.b_bank[kb];
         mk = MaskAcc();
@@ -162,11 +182,13 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         }
         if (wm) mk.store(mbase + (size_t)(kb * 4 + w) * WPL);
         __syncthreads();
+        FZ_PH();
         // in_conv over this bank block (K = 128 channels of the block)
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, T - 1);
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc_h, nf0, ring, op_inb(kb), kb + 1 < nb ? op_bank(kb + 1) : op_inx(), BK, rb);
         if (!DBUF) __syncthreads();
+        FZ_PH();
     }
     {   // in_conv, x block (K = 80)
 #pragma unroll
@@ -174,6 +196,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc_h, nf0, ring, op_inx(), op_c1(0), XB, rb);
     }
     __syncthreads();   // XB / BK are dead: HB and YB alias them
+    FZ_PH();
 
     // h0 = act(in_conv + b): fp32 residual stream in registers, operand image in HB
     f32x4 hres[2][NF];
@@ -207,6 +230,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         if (wm) mk.store(mbase + (size_t)(nb * 4 + w) * WPL);
     }
     __syncthreads();
+    FZ_PH();
 
     // one conv block (models.py:285-305); nfi / nfo: fragments of its input / output frames
     auto block = [&](auto nfi, auto nfo, int l, int Ti, int To, int s) __attribute__((always_inline)) {
@@ -216,6 +240,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, Ti - 1);
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c1(l), op_c2(l), HB, rb);
+        FZ_PH();
         mk = MaskAcc();
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -244,12 +269,14 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         }
         if (wm) mk.store(mbase + (size_t)((nb + 1 + 2 * l) * 4 + w) * WPL);
         __syncthreads();
+        FZ_PH();
         // conv2 (stride s): y2 = act(conv2(y1) + b2); h = y2 + avg_pool1d(h, s, ceil_mode)
         zero_acc(acc);
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, To - 1) * s;
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfo, ring, op_c2(l),
                                       l + 1 < nblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l)), YB, rb);
+        FZ_PH();
         if (s == 2) {
             // pooled[t'] = (h[2t'] + h[2t'+1]) / cnt : sources in frags 2f', 2f'+1; increasing f'
             // order keeps the in-place update safe (frag f' is read before it is written)
@@ -305,6 +332,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         }
         if (wm) mk.store(mbase + (size_t)((nb + 2 + 2 * l) * 4 + w) * WPL);
         __syncthreads();
+        FZ_PH();
     };
     int TN;
     if constexpr (STD != 0) {
@@ -359,6 +387,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
             *reinterpret_cast<f32x4*>(A.pooled + (size_t)b * FZ_C + ch0 + 16 * i) = m;
         }
     }
+    FZ_PH();
+    FZ_PH_DUMP("fwd");
 }
 
 // ---------------------------------------------------------------------------------
@@ -387,6 +417,8 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const int c = lane & 15, kq = lane >> 4;
     const int act = A.act;
     const int ch0 = 32 * w + 4 * kq;
+    FZ_PH_DECL
+    FZ_PH();
     const u64* mbase = A.masks + (size_t)b * A.mask_words;
     auto mword = [&](int layer, int widx) __attribute__((always_inline)) -> u64 {
         return mbase[(size_t)(layer * 4 + w) * WPL + widx];
@@ -412,6 +444,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         for (int f = 0; f < NF; ++f) gh[i][f] = (16 * f + c < TN) ? g : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();
+    FZ_PH();
 
     const int ns_c = ks * FZ_C / KS;
     const int nblk = STD ? StdSE::NBLK : A.nblk;
@@ -444,6 +477,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 }
         }
         __syncthreads();
+        FZ_PH();
         // conv2^T
         const int ncol = Ti + 2 * P;
 #pragma unroll
@@ -454,7 +488,9 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         f32x4 acc[2][NF];
         zero_acc(acc);
         fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l), op_c1T(l), GB, rb);
+        FZ_PH();
         fold_edges(acc, Ti, P, FSCR);
+        FZ_PH();
         {   // * act'(y1_l) -> GB2 (stride 1)
             const int L1 = nb + 1 + 2 * l;
 #pragma unroll
@@ -471,9 +507,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 }
         }
         __syncthreads();
+        FZ_PH();
         // conv1^T (+ fold) + avg_pool^T of g(h_{l+1}) -> g(h_l)
         zero_acc(acc);
         fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c1T(l), l > 0 ? op_c2T(l - 1) : op_c1T(l), GB2, rb);
+        FZ_PH();
         fold_edges(acc, Ti, P, FSCR);
         if (s == 2) {
             // g_h[t] += g_{l+1}[t/2] / cnt(t/2) (torch avg_pool backward: grad / divide_factor);
@@ -506,6 +544,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     gh[i][f] = t < Ti ? acc[i][f] + gh[i][f] : f32x4{0.f, 0.f, 0.f, 0.f};
                 }
         }
+        FZ_PH();
     };
     if constexpr (STD != 0) {
         static_for<0, StdSE::NBLK>([&](auto L) __attribute__((always_inline)) {
@@ -533,6 +572,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
             if (t < T) st4<PREC>(GP + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
         }
     __syncthreads();
+    FZ_PH();
 
     // bank dgrad, K split over waves: wave w sums over bank channels [32w, 32w+32) of
     // every bank kernel and produces a partial g(x) over all 80 x (T + 2*EB) columns.
@@ -566,6 +606,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         ring_fill(ring5, opx);
         fz_gemm<PREC, 5, NF, FZ_C, 1>(accx, nfx, ring5, opx, op_inTb(0), GP, rb);
     }
+    FZ_PH();
     for (int kb = 0; kb < nb; ++kb) {
         const int k = kb + 1, pl = k / 2;
         // g(b_k) for this wave's 32 bank channels = (W_in[:, kb]^T g_pre0) * act'(b_k)
@@ -575,6 +616,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
 #pragma unroll
         for (int f = 0; f < 8; ++f) rt[f] = ZP + min(16 * f + c, T - 1);
         fz_gemm<PREC, 2, 8, FZ_C, 1>(acc, nf0, ring5, op_inTb(kb), op_bankT(kb), GP, rt);
+        FZ_PH();
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -587,6 +629,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 if (t < T) st4<PREC>(GBK + (ZPB + t) * RS + (ch0 + 16 * i) * ESZ, v);
             }
         __syncthreads();
+        FZ_PH();
         // bank_k^T over this wave's channel quarter: rows q = v + pl - j of g(b_k)
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
@@ -595,8 +638,10 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         }
         fz_gemm<PREC, 5, NF, FZ_C, -1>(accx, nfx, ring5, op_bankT(kb), kb + 1 < nb ? op_inTb(kb + 1) : op_bankT(kb), GBK, rb);
         __syncthreads();
+        FZ_PH();
     }
     fold_edges(accx, T, EB, FSCR);
+    FZ_PH();
 
     // deterministic cross-wave sum: ((p0 + p2) + (p1 + p3)), then tanh' + Adam
     float* R0 = reinterpret_cast<float*>(fz_lds);
@@ -620,10 +665,13 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         }
         __syncthreads();
     }
+    FZ_PH();
 
     if (A.gx_out) {   // d loss / d x handed on (fb: the decoder output's gradient)
-        float* gx = A.gx_out + (size_t)b * FZ_CIN * T;
-        for (int idx = tid; idx < FZ_CIN * T; idx += 256) gx[idx] = R0[idx] + R1[idx];
+        f32x4* gx = reinterpret_cast<f32x4*>(A.gx_out + (size_t)b * FZ_CIN * T);
+        const f32x4* R04 = reinterpret_cast<const f32x4*>(R0);
+        const f32x4* R14 = reinterpret_cast<const f32x4*>(R1);
+        for (int q = tid; q < FZ_CIN * T / 4; q += 256) gx[q] = R04[q] + R14[q];
         return;
     }
     const AdamArgs& Ad = A.adam;
@@ -631,24 +679,54 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const int step = min(max(*A.step, 1), A.table_len);
     const float nstep = Ad.table[2 * (step - 1)];
     const float bc2s = Ad.table[2 * (step - 1) + 1];
-    const size_t base = (size_t)b * FZ_CIN * T;
-    for (int idx = tid; idx < FZ_CIN * T; idx += 256) {
-        const size_t o = base + idx;
-        const float gsum = R0[idx] + R1[idx];
-        float p = Ad.ptb[o];
-        const float th = tanhf(p);
-        const float g = (gsum * eps) * (1.f - th * th);
-        if (Ad.grad0 && step == 1) Ad.grad0[o] = g;
-        float mm = Ad.m[o];
-        mm = mm + Ad.b1c * (g - mm);
-        float vv = Ad.v[o] * Ad.b2;
-        vv = vv + Ad.b2c * g * g;
-        p = p + nstep * (mm / (sqrtf(vv) / bc2s + Ad.adam_eps));
-        Ad.ptb[o] = p;
-        Ad.m[o] = mm;
-        Ad.v[o] = vv;
-        Ad.adv[o] = Ad.vc[o] + eps * tanhf(p);
+    const size_t base4 = (size_t)b * FZ_CIN * T / 4;
+    f32x4* __restrict__ ptb4 = reinterpret_cast<f32x4*>(Ad.ptb) + base4;
+    f32x4* __restrict__ m4 = reinterpret_cast<f32x4*>(Ad.m) + base4;
+    f32x4* __restrict__ v4 = reinterpret_cast<f32x4*>(Ad.v) + base4;
+    const f32x4* __restrict__ vc4 = reinterpret_cast<const f32x4*>(Ad.vc) + base4;
+    f32x4* __restrict__ adv4 = reinterpret_cast<f32x4*>(Ad.adv) + base4;
+    f32x4* __restrict__ g04 = Ad.grad0 && step == 1 ? reinterpret_cast<f32x4*>(Ad.grad0) + base4 : nullptr;
+    const f32x4* R04 = reinterpret_cast<const f32x4*>(R0);
+    const f32x4* R14 = reinterpret_cast<const f32x4*>(R1);
+    // 16-byte accesses; a batch's loads all issued before its arithmetic (one HBM round
+    // trip per batch instead of one per element)
+    const int n4 = FZ_CIN * T / 4;
+    constexpr int AB = 5;                       // f32x4 per thread per batch
+    for (int q0 = 0; q0 < n4; q0 += 256 * AB) {
+        f32x4 P[AB], M[AB], V[AB], X[AB];
+#pragma unroll
+        for (int k = 0; k < AB; ++k) {
+            const int q = min(q0 + tid + 256 * k, n4 - 1);
+            P[k] = ptb4[q];
+            M[k] = m4[q];
+            V[k] = v4[q];
+            X[k] = vc4[q];
+        }
+#pragma unroll
+        for (int k = 0; k < AB; ++k) {
+            const int q = q0 + tid + 256 * k;
+            if (q >= n4) continue;
+            const f32x4 gsum = R04[q] + R14[q];
+            f32x4 p = P[k], mm = M[k], vv = V[k], g, ad;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float th = tanhf(p[e]);
+                g[e] = (gsum[e] * eps) * (1.f - th * th);
+                mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
+                vv[e] = vv[e] * Ad.b2;
+                vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
+                p[e] = p[e] + nstep * (mm[e] / (sqrtf(vv[e]) / bc2s + Ad.adam_eps));
+                ad[e] = X[k][e] + eps * tanhf(p[e]);
+            }
+            if (g04) g04[q] = g;
+            ptb4[q] = p;
+            m4[q] = mm;
+            v4[q] = vv;
+            adv4[q] = ad;
+        }
     }
+    FZ_PH();
+    FZ_PH_DUMP("bwd");
 }
 
 #define AVC_FZ_INST(P, S)                                        \

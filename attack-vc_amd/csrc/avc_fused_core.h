@@ -246,6 +246,32 @@ __device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing
             R.a[u][i] = rem == 1 ? t[(u + 1) & 3][i] : (rem == 2 ? t[(u + 2) & 3][i] : t[(u + 3) & 3][i]);
 }
 
+// Diagnostic build only (-DAVC_FZ_PHASES): per-wave cycle stamps at phase boundaries,
+// printed by workgroup 0 at the end of the kernel (scripts/dbg/phases.sh).
+#ifdef AVC_FZ_PHASES
+#define FZ_PH_DECL          \
+    unsigned long long fz_ph[96]; \
+    int fz_phn = 0;
+#define FZ_PH()                                                            \
+    do {                                                                   \
+        if (fz_phn < 96) fz_ph[fz_phn++] = __builtin_readcyclecounter();   \
+    } while (0)
+#define FZ_PH_DUMP(tag)                                                                            \
+    do {                                                                                           \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0)                                            \
+            for (int i_ = 1; i_ < fz_phn; ++i_)                                                    \
+                printf("%s w%d %d %llu\n", tag, (int)(threadIdx.x >> 6), i_, fz_ph[i_] - fz_ph[i_ - 1]); \
+    } while (0)
+#else
+#define FZ_PH_DECL
+#define FZ_PH() \
+    do {        \
+    } while (0)
+#define FZ_PH_DUMP(tag) \
+    do {                \
+    } while (0)
+#endif
+
 template <int V>
 using IC = std::integral_constant<int, V>;
 

@@ -377,14 +377,17 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     // C == D == 128 (fused engine): every step is a 128 x 128 matrix, K/4 = 32 weights
     // per thread -- eight unconditional 16-byte loads, no branches for the waitcnt
     // pass to be conservative about
+    // (host layout: chunk e of thread t at float ((t/64*8 + e)*64 + t%64)*4 of the step's
+    // matrix, so every load instruction of a wave reads one contiguous 1 KiB run)
+    const int wv = tid >> 6, ln = tid & 63;
     auto load_w = [&](HeadVW& hw, int i) __attribute__((always_inline)) {
-        const float* row = step_w(i) + (size_t)m * 128 + q * 32;
+        const float* base = step_w(i) + ((size_t)wv * 8 * 64 + ln) * 4;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
 #if AVC_HEAD_ABLATE & 1
             hw.w[e] = f32x4{0.01f * i, 0.02f, 0.03f, 0.04f * e};
 #else
-            hw.w[e] = gload<f32x4>(row + 4 * e);
+            hw.w[e] = gload<f32x4>(base + (size_t)e * 64 * 4);
 #endif
         }
     };
