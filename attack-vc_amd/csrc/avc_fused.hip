@@ -152,9 +152,17 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     f32x4 acc_h[2][NF];
     zero_acc(acc_h);
     MaskAcc mk;
+    // biases are loaded ahead of the GEMM that precedes their epilogue (their latency
+    // then hides under it instead of stalling the epilogue)
+    f32x4 b_in[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) b_in[i] = *reinterpret_cast<const f32x4*>(A.w.b_in + ch0 + 16 * i);
     for (int kb = 0; kb < nb; ++kb) {
         const int k = kb + 1;
         const int pl = k / 2;
+        f32x4 bkb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) bkb[i] = *reinterpret_cast<const f32x4*>(A.w.b_bank[kb] + ch0 + 16 * i);
         f32x4 acc[2][NF];
         zero_acc(acc);
 #pragma unroll
@@ -162,11 +170,10 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc, nf0, ring, op_bank(kb), op_inb(kb), XB, rb);
         FZ_PH();
         char* BK = (kb & 1) ? BK1 : BK0;
-        const float* bias = A.w.b_bank[kb];
         mk = MaskAcc();
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const f32x4 bi = *reinterpret_cast<const f32x4*>(bias + ch0 + 16 * i);
+            const f32x4 bi = bkb[i];
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 if (f >= nf0) continue;
@@ -204,9 +211,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         mk = MaskAcc();
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_in + ch0 + 16 * i);
 #pragma unroll
-            for (int f = 0; f < NF; ++f) acc_h[i][f] += bi;
+            for (int f = 0; f < NF; ++f) acc_h[i][f] += b_in[i];
         }
         if (ce) {   // ContentEncoder: InstanceNorm before the act (models.py:199-200)
             f32x4 is[2];
@@ -235,6 +241,12 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     // one conv block (models.py:285-305); nfi / nfo: fragments of its input / output frames
     auto block = [&](auto nfi, auto nfo, int l, int Ti, int To, int s) __attribute__((always_inline)) {
         f32x4 acc[2][NF];
+        f32x4 bc1[2], bc2[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            bc1[i] = *reinterpret_cast<const f32x4*>(A.w.b_c1[l] + ch0 + 16 * i);
+            bc2[i] = *reinterpret_cast<const f32x4*>(A.w.b_c2[l] + ch0 + 16 * i);
+        }
         // conv1 (stride 1): y1 = act(conv1(h) + b1) -> YB
         zero_acc(acc);
 #pragma unroll
@@ -244,9 +256,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         mk = MaskAcc();
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_c1[l] + ch0 + 16 * i);
 #pragma unroll
-            for (int f = 0; f < NF; ++f) acc[i][f] += bi;
+            for (int f = 0; f < NF; ++f) acc[i][f] += bc1[i];
         }
         if (ce) {
             f32x4 is[2];
@@ -305,9 +316,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         mk = MaskAcc();
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_c2[l] + ch0 + 16 * i);
 #pragma unroll
-            for (int f = 0; f < NF; ++f) acc[i][f] += bi;
+            for (int f = 0; f < NF; ++f) acc[i][f] += bc2[i];
         }
         if (ce) {
             f32x4 is[2];
@@ -420,9 +430,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     FZ_PH_DECL
     FZ_PH();
     const u64* mbase = A.masks + (size_t)b * A.mask_words;
-    auto mword = [&](int layer, int widx) __attribute__((always_inline)) -> u64 {
-        return mbase[(size_t)(layer * 4 + w) * WPL + widx];
-    };
+    auto mwords = [&](int layer) __attribute__((always_inline)) { return mbase + (size_t)(layer * 4 + w) * WPL; };
 
     char* GB = fz_lds;                          // dilated dY image [T+2ZP] rows
     char* GB2 = GB + (T + 2 * ZP) * RS;         // stride-1 dY image [T+2ZP] rows
@@ -453,12 +461,14 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     ARing<2> ring;
     ring_fill(ring, op_c2T(nblk - 1));
     int rb[NF];
+    // ReLU' words of the next layer whose mask is applied, loaded one GEMM ahead
+    MaskRd mnext;
+    mnext.load(mwords(nb + 2 + 2 * (nblk - 1)));
     // backward of one conv block; nfo: fragments of its output frames, nfc: of the
     // dgrad columns (Ti interior frames + 2P pad positions)
     auto block = [&](auto nfo, auto nfc, int l, int Ti, int To, int s) __attribute__((always_inline)) {
         // dY of conv2 = g(h_{l+1}) * act'(y2_l), written dilated by s into GB
         {
-            const int L2 = nb + 2 + 2 * l;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -467,7 +477,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     f32x4 v;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        v[r] = gh[i][f][r] * act_bit(mword(L2, (i * FZ_MAXNF + f) * 4 + r), lane, act);
+                        v[r] = gh[i][f][r] * act_bit(mnext.word((i * FZ_MAXNF + f) * 4 + r), lane, act);
                     const int t = 16 * f + c;
                     if (t < To) {
                         st4<PREC>(GB + (ZP + s * t) * RS + (ch0 + 16 * i) * ESZ, v);
@@ -487,12 +497,13 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         }
         f32x4 acc[2][NF];
         zero_acc(acc);
+        MaskRd m1;
+        m1.load(mwords(nb + 1 + 2 * l));
         fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l), op_c1T(l), GB, rb);
         FZ_PH();
         fold_edges(acc, Ti, P, FSCR);
         FZ_PH();
         {   // * act'(y1_l) -> GB2 (stride 1)
-            const int L1 = nb + 1 + 2 * l;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -501,7 +512,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     f32x4 v;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        v[r] = acc[i][f][r] * act_bit(mword(L1, (i * FZ_MAXNF + f) * 4 + r), lane, act);
+                        v[r] = acc[i][f][r] * act_bit(m1.word((i * FZ_MAXNF + f) * 4 + r), lane, act);
                     const int t = 16 * f + c;
                     if (t < Ti) st4<PREC>(GB2 + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
                 }
@@ -510,6 +521,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         FZ_PH();
         // conv1^T (+ fold) + avg_pool^T of g(h_{l+1}) -> g(h_l)
         zero_acc(acc);
+        mnext.load(mwords(l > 0 ? nb + 2 + 2 * (l - 1) : nb));   // next block's conv2, or h0
         fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c1T(l), l > 0 ? op_c2T(l - 1) : op_c1T(l), GB2, rb);
         FZ_PH();
         fold_edges(acc, Ti, P, FSCR);
@@ -567,7 +579,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
             if (f >= nf0) continue;
             f32x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = gh[i][f][r] * act_bit(mword(nb, (i * FZ_MAXNF + f) * 4 + r), lane, act);
+            for (int r = 0; r < 4; ++r) v[r] = gh[i][f][r] * act_bit(mnext.word((i * FZ_MAXNF + f) * 4 + r), lane, act);
             const int t = 16 * f + c;
             if (t < T) st4<PREC>(GP + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
         }
@@ -612,6 +624,8 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         // g(b_k) for this wave's 32 bank channels = (W_in[:, kb]^T g_pre0) * act'(b_k)
         f32x4 acc[2][8];
         zero_acc(acc);
+        MaskRd mb;
+        mb.load(mwords(kb));
         int rt[8];
 #pragma unroll
         for (int f = 0; f < 8; ++f) rt[f] = ZP + min(16 * f + c, T - 1);
@@ -624,7 +638,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 if (f >= nf0) continue;
                 f32x4 v;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] * act_bit(mword(kb, (i * FZ_MAXNF + f) * 4 + r), lane, act);
+                for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] * act_bit(mb.word((i * FZ_MAXNF + f) * 4 + r), lane, act);
                 const int t = 16 * f + c;
                 if (t < T) st4<PREC>(GBK + (ZPB + t) * RS + (ch0 + 16 * i) * ESZ, v);
             }

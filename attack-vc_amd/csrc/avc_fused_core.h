@@ -399,6 +399,25 @@ struct MaskAcc {
     }
 };
 
+// The same words read back for a backward pass: one coalesced vector load per (layer,
+// wave) issued ahead of the GEMM that precedes their use (lane j holds words j and
+// 64 + j); word(widx) with a compile-time widx is two v_readlane.
+struct MaskRd {
+    u64 lo = 0, hi = 0;
+    __device__ __forceinline__ void load(const u64* base) {
+        const int lane = threadIdx.x & 63;
+        lo = base[lane];
+        hi = lane < FZ_MASK_WORDS_PER_LAYER / 4 - 64 ? base[64 + lane] : 0ull;
+    }
+    __device__ __forceinline__ u64 word(int widx) const {
+        const u64 v = widx < 64 ? lo : hi;
+        const int l = widx & 63;
+        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+        const unsigned b = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+        return ((u64)b << 32) | a;
+    }
+};
+
 __device__ __forceinline__ float act_bit(u64 word, int lane, int act) {
     return ((word >> lane) & 1ull) ? 1.f : (act ? 0.01f : 0.f);
 }
