@@ -1050,7 +1050,7 @@ static FusedArgs fused_args(avc_ctx* ctx, Workspace& ws, int prec) {
 // compile-time), else the fragment bound 1|2|4|8 >= ceil(T/16)
 static int fused_shape(avc_ctx* ctx, int T) {
     const avc_se_cfg& c = ctx->cfg;
-    bool std_cfg = T == 128 && ctx->nb == 8 && c.kernel_size == 5 && c.n_conv_blocks == 6;
+    bool std_cfg = T == 128 && ctx->nb == 8 && c.kernel_size == 5 && c.n_conv_blocks == 6 && c.act == 0;
     for (int l = 0; std_cfg && l < 6; ++l)
         if (c.subsample[l] != ((l & 1) ? 2 : 1)) std_cfg = false;
     const char* e = getenv("AVC_FUSED_STD");

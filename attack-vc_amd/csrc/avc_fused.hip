@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
-    const int act = A.act;
+    const int act = STD ? 0 : A.act;                   // the standard shape is ReLU (host-checked)
     FZ_PH_DECL
     FZ_PH();
     if (A.tick && b == 0 && tid == 0) atomicAdd(A.tick, 1);
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = act_f(acc[i][f][r] + bi[r], act);
-                    mk.put((i * FZ_MAXNF + f) * 4 + r, __ballot(y[r] > 0.f));
+                    mk.put(i, f, r, y[r] > 0.f);
                 }
                 const int t = 16 * f + c;
                 if (t < T) st4<PREC>(BK + t * RS + (ch0 + 16 * i) * ESZ, y);
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = act_f(acc_h[i][f][r], act);
-                    mk.put((i * FZ_MAXNF + f) * 4 + r, __ballot(y[r] > 0.f));
+                    mk.put(i, f, r, y[r] > 0.f);
                 }
                 hres[i][f] = y;
                 const int t = 16 * f + c;
@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = act_f(acc[i][f][r], act);
-                    mk.put((i * FZ_MAXNF + f) * 4 + r, __ballot(y[r] > 0.f));
+                    mk.put(i, f, r, y[r] > 0.f);
                 }
                 const int t = 16 * f + c;
                 if (t < Ti) put_reflect<PREC>(YB, t, Ti, P, (ch0 + 16 * i) * ESZ, y);
@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = act_f(acc[i][f][r], act);
-                    mk.put((i * FZ_MAXNF + f) * 4 + r, __ballot(y[r] > 0.f));
+                    mk.put(i, f, r, y[r] > 0.f);
                     h[r] = y[r] + hres[i][f][r];
                 }
                 hres[i][f] = h;
@@ -425,7 +425,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
-    const int act = A.act;
+    const int act = STD ? 0 : A.act;                   // the standard shape is ReLU (host-checked)
     const int ch0 = 32 * w + 4 * kq;
     FZ_PH_DECL
     FZ_PH();
@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     f32x4 v;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        v[r] = gh[i][f][r] * act_bit(mnext.word((i * FZ_MAXNF + f) * 4 + r), lane, act);
+                        v[r] = gh[i][f][r] * mnext.act(i, f, r, act);
                     const int t = 16 * f + c;
                     if (t < To) {
                         st4<PREC>(GB + (ZP + s * t) * RS + (ch0 + 16 * i) * ESZ, v);
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     f32x4 v;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        v[r] = acc[i][f][r] * act_bit(m1.word((i * FZ_MAXNF + f) * 4 + r), lane, act);
+                        v[r] = acc[i][f][r] * m1.act(i, f, r, act);
                     const int t = 16 * f + c;
                     if (t < Ti) st4<PREC>(GB2 + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
                 }
@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
             if (f >= nf0) continue;
             f32x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = gh[i][f][r] * act_bit(mnext.word((i * FZ_MAXNF + f) * 4 + r), lane, act);
+            for (int r = 0; r < 4; ++r) v[r] = gh[i][f][r] * mnext.act(i, f, r, act);
             const int t = 16 * f + c;
             if (t < T) st4<PREC>(GP + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
         }
@@ -638,7 +638,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 if (f >= nf0) continue;
                 f32x4 v;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] * act_bit(mb.word((i * FZ_MAXNF + f) * 4 + r), lane, act);
+                for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] * mb.act(i, f, r, act);
                 const int t = 16 * f + c;
                 if (t < T) st4<PREC>(GBK + (ZPB + t) * RS + (ch0 + 16 * i) * ESZ, v);
             }

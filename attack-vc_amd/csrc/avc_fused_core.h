@@ -379,48 +379,38 @@ __device__ __forceinline__ void inorm_rows(f32x4 (&v)[MT][NF], int nf, int T, f3
     }
 }
 
-// 64-bit ReLU' ballot words of one layer for this wave: word (i*FZ_MAXNF + f)*4 + r
-// lives in lane word%64 of lo (words < 64) or hi (words >= 64)
+// ReLU' masks of one layer for this wave, per lane: bit 4f + r of word i is
+// (y[i][f][r] > 0) for this lane's element (tile i, fragment f < 8, row r).  Built with
+// lane-local ops only and stored as one u64 per lane (lo = tile 0, hi = tile 1): a
+// coalesced 512-B row per (layer, wave); the backward reads its own lane's word back.
 struct MaskAcc {
-    u64 lo = 0, hi = 0;
-    __device__ __forceinline__ void put(int widx, u64 word) {
+    unsigned lo = 0, hi = 0;
+    __device__ __forceinline__ void put(int i, int f, int r, bool pos) {
         if (AVC_FZ_ABLATE & 2) return;
-        const int lane = threadIdx.x & 63;
-        if (widx < 64) {
-            if (lane == widx) lo = word;
-        } else {
-            if (lane == widx - 64) hi = word;
-        }
+        const unsigned bit = pos ? (1u << (4 * f + r)) : 0u;
+        if (i == 0) lo |= bit;
+        else hi |= bit;
     }
     __device__ __forceinline__ void store(u64* base) const {
-        const int lane = threadIdx.x & 63;
-        base[lane] = lo;
-        if (lane < FZ_MASK_WORDS_PER_LAYER / 4 - 64) base[64 + lane] = hi;
+        base[threadIdx.x & 63] = ((u64)hi << 32) | lo;
     }
 };
 
-// The same words read back for a backward pass: one coalesced vector load per (layer,
-// wave) issued ahead of the GEMM that precedes their use (lane j holds words j and
-// 64 + j); word(widx) with a compile-time widx is two v_readlane.
+// The same words read back for a backward pass: one coalesced load per (layer, wave),
+// issued ahead of the GEMM that precedes their use.
 struct MaskRd {
-    u64 lo = 0, hi = 0;
+    unsigned lo = 0, hi = 0;
     __device__ __forceinline__ void load(const u64* base) {
-        const int lane = threadIdx.x & 63;
-        lo = base[lane];
-        hi = lane < FZ_MASK_WORDS_PER_LAYER / 4 - 64 ? base[64 + lane] : 0ull;
+        const u64 v = base[threadIdx.x & 63];
+        lo = (unsigned)v;
+        hi = (unsigned)(v >> 32);
     }
-    __device__ __forceinline__ u64 word(int widx) const {
-        const u64 v = widx < 64 ? lo : hi;
-        const int l = widx & 63;
-        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
-        const unsigned b = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
-        return ((u64)b << 32) | a;
+    // act'(y) of element (i, f, r): 1 where y > 0, else 0 (ReLU) or 0.01 (LeakyReLU)
+    __device__ __forceinline__ float act(int i, int f, int r, int actk) const {
+        const unsigned w = i == 0 ? lo : hi;
+        return ((w >> (4 * f + r)) & 1u) ? 1.f : (actk ? 0.01f : 0.f);
     }
 };
-
-__device__ __forceinline__ float act_bit(u64 word, int lane, int act) {
-    return ((word >> lane) & 1ull) ? 1.f : (act ? 0.01f : 0.f);
-}
 
 // write 4 consecutive channels of frame t of a padded operand image (pad P rows each
 // side, reflect): row P+t, plus its mirror rows (F.pad reflect)

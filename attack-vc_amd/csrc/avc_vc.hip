@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
     const int ch0 = 32 * w + 4 * kq;
-    const int act = A.act;
+    const int act = STD ? 0 : A.act;                   // the standard shape is ReLU (host-checked)
     const float* cond = A.cond + (size_t)b * (2 * nblk) * 256;
     const bool stash = A.stash_per_utt > 0;
 
@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
     const int ch0 = 32 * w + 4 * kq;
-    const int act = A.act;
+    const int act = STD ? 0 : A.act;                   // the standard shape is ReLU (host-checked)
     const float* cond = A.cond + (size_t)b * (2 * nblk) * 256;
     float* gcond = A.g_cond + (size_t)b * (2 * nblk) * 256;
 
