@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
 // e < 2) -- stored contiguously by the host packer (Wr/WrT are row-permuted) -- so the
 // four slices of a row read adjacent 16-byte chunks of the [k][utterance] input
 // (conflict-free, broadcast over the 16 rows of a wave).  Its 2 partial dot products
-// are summed over q with two xor-shuffles.  Weights are fetched four steps ahead (each
+// are summed over q with two DPP quad moves.  Weights are fetched three steps ahead (each
 // step otherwise waits a full MALL round trip).
 // Modes: 0 = forward (EMB -> emb_out); 1 = emb attack (loss vs tgt/org, backward ->
 // g_pooled); 3 = backward from a given d loss / d EMB (passed as `tgt`) -> g_pooled.
@@ -302,6 +302,12 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
 //   j odd            : GB += W_{2l}^T GA;      GM = GB * act'(Y_{2l-1})  (l > 0)
 // ---------------------------------------------------------------------------------
 constexpr int HV = 2;
+
+// v_mov_b32 with a DPP quad permutation: 0xB1 = [1,0,3,2] (lane ^ 1), 0x4E = [2,3,0,1] (lane ^ 2)
+template <int CTRL>
+__device__ __forceinline__ float quad_xor(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 #ifndef AVC_HEAD_ABLATE
 #define AVC_HEAD_ABLATE 0
 #endif
@@ -416,8 +422,9 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
         acc[1] = acc[1] + acc2[1];
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            acc[r] += __shfl_xor(acc[r], 1);
-            acc[r] += __shfl_xor(acc[r], 2);
+            // quad reductions on DPP (lane ^ 1, lane ^ 2 within the 4 slices of a row)
+            acc[r] += quad_xor<0xB1>(acc[r]);
+            acc[r] += quad_xor<0x4E>(acc[r]);
         }
         return acc;
     };
@@ -442,11 +449,11 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     const float gscale = A.scal[1];
     const int step_no = mode == 0 ? 0 : *A.step;
     __syncthreads();
-    HeadVW w0, w1, w2, w3;
+    // 3-step register ring (8 waves = 2 per SIMD cap a wave at 256 registers; a 4th slot spilled)
+    HeadVW w0, w1, w2;
     load_w(w0, 0);
     load_w(w1, min(1, NL - 1));
     load_w(w2, min(2, NL - 1));
-    load_w(w3, min(3, NL - 1));
 
     auto run_step = [&](int i, const HeadVW& hw) __attribute__((always_inline)) {
         constexpr int K = 128;
@@ -539,24 +546,21 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
         __syncthreads();
     };
 
-    // static 4-step register ring: slot u holds step i+u and is refilled with step
-    // i+4+u right after its step.  Refills are unconditional (clamped to the last step)
+    // static 3-step register ring: slot u holds step i+u and is refilled with step
+    // i+3+u right after its step.  Refills are unconditional (clamped to the last step)
     // and the loop has no early exits: on a conditional path the waitcnt pass would
     // have to assume the newest loads are the ones awaited and drain the whole ring.
-    const int nfull = NL & ~3;
-    for (int i = 0; i < nfull; i += 4) {
+    const int nfull = NL - NL % 3;
+    for (int i = 0; i < nfull; i += 3) {
         run_step(i, w0);
-        load_w(w0, min(i + 4, NL - 1));
+        load_w(w0, min(i + 3, NL - 1));
         run_step(i + 1, w1);
-        load_w(w1, min(i + 5, NL - 1));
+        load_w(w1, min(i + 4, NL - 1));
         run_step(i + 2, w2);
-        load_w(w2, min(i + 6, NL - 1));
-        run_step(i + 3, w3);
-        load_w(w3, min(i + 7, NL - 1));
+        load_w(w2, min(i + 5, NL - 1));
     }
     if (NL - nfull > 0) run_step(nfull, w0);
     if (NL - nfull > 1) run_step(nfull + 1, w1);
-    if (NL - nfull > 2) run_step(nfull + 2, w2);
     if (mode == 1 && losses && step_no >= 1 && step_no <= loss_len && tid < HV) {
         const int b = u0 + tid;
         if (b < Bn) losses[(size_t)(step_no - 1) * Bn + b] = LS[tid];
