@@ -386,10 +386,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
         for (int f = 0; f < NF; ++f)
             if (16 * f + c < TN) s4 += hres[i][f];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s4[r] += __shfl_xor(s4[r], o);
+        row16_sum(s4);
         if (c == 0) {
             f32x4 m;
 #pragma unroll

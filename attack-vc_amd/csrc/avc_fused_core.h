@@ -341,6 +341,26 @@ __device__ __forceinline__ void fold_edges(f32x4 (&acc)[MT][NF], int Tin, int E,
     }
 }
 
+// Sum over the 16 lanes of each row (lane group) of a wave, every lane receiving the
+// result, on DPP moves (no LDS round trip): rotate by 8 and 4 inside the row, then the
+// quad permutations lane^2 and lane^1.  Each step adds (own + partner) == (partner + own),
+// so all 16 lanes hold bitwise the same sum.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_mov<0x128>(v);   // row_ror:8
+    v += dpp_mov<0x124>(v);   // row_ror:4
+    v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+    return v;
+}
+__device__ __forceinline__ void row16_sum(f32x4& v) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = row16_sum(v[r]);
+}
+
 // InstanceNorm1d (affine=False, eps 1e-5; models.py:176,396) of the rows this wave owns:
 // row (i, r) of v is one channel over the frames t = 16f + c < T (lanes of a 16-lane
 // group x fragments).  Two-pass mean / biased variance like ATen's batch_norm_cpu
@@ -354,10 +374,7 @@ __device__ __forceinline__ void inorm_rows(f32x4 (&v)[MT][NF], int nf, int T, f3
 #pragma unroll
         for (int f = 0; f < NF; ++f)
             if (f < nf && 16 * f + c < T) s += v[i][f];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o);
+        row16_sum(s);
         f32x4 mean;
 #pragma unroll
         for (int r = 0; r < 4; ++r) mean[r] = s[r] / (float)T;
@@ -368,10 +385,7 @@ __device__ __forceinline__ void inorm_rows(f32x4 (&v)[MT][NF], int nf, int T, f3
                 const f32x4 d = v[i][f] - mean;
                 q += d * d;
             }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) q[r] += __shfl_xor(q[r], o);
+        row16_sum(q);
 #pragma unroll
         for (int r = 0; r < 4; ++r) invstd[i][r] = 1.f / sqrtf(q[r] / (float)T + 1e-5f);
 #pragma unroll

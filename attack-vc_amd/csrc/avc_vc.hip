@@ -56,10 +56,7 @@ __device__ __forceinline__ void inorm_rows2(f32x4 (&v0)[2][NF], f32x4 (&v1)[2][N
 #pragma unroll
         for (int f = 0; f < NF; ++f)
             if (f < nf && 16 * f + c < T) s += v0[i][f] + v1[i][f];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o);
+        row16_sum(s);
         f32x4 mean;
 #pragma unroll
         for (int r = 0; r < 4; ++r) mean[r] = s[r] / (float)(2 * T);
@@ -70,10 +67,7 @@ __device__ __forceinline__ void inorm_rows2(f32x4 (&v0)[2][NF], f32x4 (&v1)[2][N
                 const f32x4 d0 = v0[i][f] - mean, d1 = v1[i][f] - mean;
                 q += d0 * d0 + d1 * d1;
             }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) q[r] += __shfl_xor(q[r], o);
+        row16_sum(q);
 #pragma unroll
         for (int r = 0; r < 4; ++r) invstd[i][r] = 1.f / sqrtf(q[r] / (float)(2 * T) + 1e-5f);
 #pragma unroll
@@ -92,10 +86,7 @@ __device__ __forceinline__ f32x4 row_sum(const f32x4 (&v)[NF], int nf, int T) {
 #pragma unroll
     for (int f = 0; f < NF; ++f)
         if (f < nf && 16 * f + c < T) s += v[f];
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o);
+    row16_sum(s);
     return s;
 }
 
@@ -501,13 +492,8 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
                     }
                 }
             }
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    gm[r] += __shfl_xor(gm[r], o);
-                    gs[r] += __shfl_xor(gs[r], o);
-                }
+            row16_sum(gm);
+            row16_sum(gs);
             if (c == 0) {
                 *reinterpret_cast<f32x4*>(gcond + q * 256 + ch0 + 16 * i) = gm;
                 *reinterpret_cast<f32x4*>(gcond + q * 256 + 128 + ch0 + 16 * i) = gs;
