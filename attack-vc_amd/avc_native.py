@@ -73,6 +73,13 @@ SIGNATURES = [
     ("avc_fb_attack", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                      ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_pm_weight_count", ctypes.c_size_t, []),
+    ("avc_pm_create", ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    ("avc_pm_destroy", None, [ctypes.c_void_p]),
+    ("avc_pm_out_shape", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                        ctypes.POINTER(ctypes.c_int)]),
+    ("avc_pm_forward", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_set_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_get_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -362,3 +369,65 @@ def vc_context_for(model: torch.nn.Module, device: torch.device) -> Context:
         ctx.attach_vc(ce_config(model.content_encoder), dec_config(model.decoder), flat)
         ctx._vc_version = version
     return ctx
+
+
+class PMContext:
+    """libavc PredictiveModel (VSMask predictor) weights on one device (avc_pm_*)."""
+
+    def __init__(self, flat: torch.Tensor, device: int):
+        w = flat.detach().to("cpu", torch.float32).contiguous()
+        need = lib().avc_pm_weight_count()
+        if w.numel() != need:
+            raise RuntimeError(f"PredictiveModel weights: got {w.numel()} values, need {need}")
+        h = ctypes.c_void_p()
+        _check(lib().avc_pm_create(int(device), ctypes.c_void_p(w.data_ptr()), w.numel(), ctypes.byref(h)))
+        self.h = h
+        self._lock = threading.Lock()
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.avc_pm_destroy(h)
+            self.h = None
+
+    @staticmethod
+    def out_shape(H: int, W: int) -> Tuple[int, int]:
+        ho, wo = ctypes.c_int(), ctypes.c_int()
+        _check(lib().avc_pm_out_shape(int(H), int(W), ctypes.byref(ho), ctypes.byref(wo)))
+        return ho.value, wo.value
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _require_gpu(x)
+        x = x.contiguous()
+        if x.dim() != 4 or x.shape[1] != 1:
+            raise RuntimeError(f"PredictiveModel expects [B, 1, F, T], got {tuple(x.shape)}")
+        B, _, H, W = x.shape
+        ho, wo = self.out_shape(H, W)
+        y = torch.empty(B, 1, ho, wo, device=x.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_pm_forward(self.h, ctypes.c_void_p(x.data_ptr()), B, H, W,
+                                        ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(stream)))
+        return y
+
+
+def pm_flat_weights(model: torch.nn.Module) -> torch.Tensor:
+    """Floating tensors of a PredictiveModel state_dict in order (num_batches_tracked excluded)."""
+    return torch.cat([v.detach().reshape(-1).to("cpu", torch.float32) for v in model.state_dict().values()
+                      if v.is_floating_point()])
+
+
+def predictive_forward(model: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """PredictiveModel.forward (models/predictive_model.py:87-110), eval semantics, on the MI355X."""
+    _require_gpu(x)
+    if model.training:
+        raise RuntimeError("libavc implements PredictiveModel inference (eval mode: BatchNorm running "
+                           "statistics); call model.eval() first")
+    dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
+    version = tuple((t.data_ptr(), t._version) for t in model.state_dict().values())
+    per = _ctx_cache.setdefault(model, {})
+    hit = per.get(("pm", dev))
+    if hit is None or hit[0] != version:
+        hit = (version, PMContext(pm_flat_weights(model), dev))
+        per[("pm", dev)] = hit
+    return hit[1].forward(x)

@@ -35,6 +35,8 @@ __global__ void dec_fwd_fused(DecArgs A);
 template <int PREC, int SH>
 __global__ void dec_bwd_fused(DecArgs A);
 __global__ void dense_batched(DenseArgs D);
+__global__ void pm_conv(PmConvArgs P);
+__global__ void pm_reduce(PmConvArgs P);
 }  // namespace avc
 #include "avc_fused_lds.h"
 
@@ -1668,3 +1670,4 @@ extern "C" int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len,
 }
 
 #include "avc_vc_host.inc"
+#include "avc_pm_host.inc"

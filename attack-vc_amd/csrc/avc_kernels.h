@@ -225,4 +225,20 @@ struct DenseArgs {
     int32_t M, K, B, kchunk;
 };
 
+// VSMask PredictiveModel layer (avc_pm.hip): implicit GEMM over NCHW activations.
+struct PmConvArgs {
+    const float* x;                   // [B][Cin][Hin][Win]
+    const float* w;                   // packed A: mode 0 [Cout][Cin*9] (BN folded); mode 1 class c at woff[c]:
+                                      // [Cout][Cin*nty*ntx]
+    const float* bias;                // [Cout]
+    float* y;                         // [B][Cout][Ho][Wo]
+    int32_t B, Cin, Hin, Win, Cout, Ho, Wo, sh, sw;
+    int32_t mode;                     // 0: reflect-pad conv 3x3 stride (sh, sw); 1: ConvTranspose2d 3x3 s2
+    int32_t act;                      // 0: PReLU(slope); 1: LeakyReLU(0.2); 2: LeakyReLU(0.2) then tanh
+    float slope;
+    int32_t woff[4];
+    int32_t ksplit;                   // > 1: K slices (blockIdx.z = class * ksplit + slice) write raw
+    float* part;                      //      partial sums to part[slice][B*Cout*Ho*Wo]; pm_reduce finishes
+};
+
 }  // namespace avc

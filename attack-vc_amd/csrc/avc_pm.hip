@@ -1,0 +1,162 @@
+// VSMask PredictiveModel forward (/root/reference/models/predictive_model.py:6-110,
+// BASELINE config 5) on gfx950: every layer is one implicit-GEMM launch
+//   Y[Cout][n] = A[Cout][K] . B[K][n],  n = (window, output pixel)
+// with B gathered on the fly from the NCHW activation:
+//   mode 0  ReflectionPad2d(1) + Conv2d 3x3 stride (sh, sw): K = (ci, ky, kx), reflect
+//           indexing of the input (the pad is never materialised); BatchNorm2d (eval)
+//           folded into A and the bias on the host; PReLU (one slope) in the epilogue.
+//   mode 1  ConvTranspose2d 3x3 stride 2 as four gather convolutions, one per output
+//           parity class (oy & 1, ox & 1) = blockIdx.z: class (py, px) only meets taps
+//           ky = 2a (py = 0, a = 0, 1) or 1 (py = 1), likewise kx, at input rows
+//           qy - a (py = 0) / qy (py = 1) -- no multiply by an inserted zero.
+//           LeakyReLU(0.2) (+ tanh on the last layer) in the epilogue.
+// fp32 FMA on the VALU (the fp32 VALU and matrix rates are equal on gfx950): 64 x 64
+// output tile per 256-thread workgroup, 4 x 4 per thread, K in chunks of 16 staged
+// through LDS.
+#include <hip/hip_runtime.h>
+
+#include "avc_kernels.h"
+
+namespace avc {
+
+__device__ __forceinline__ float pm_act(float v, const PmConvArgs& P) {
+    if (P.act == 0) return v >= 0.f ? v : P.slope * v;                // PReLU
+    v = v >= 0.f ? v : 0.2f * v;                                      // LeakyReLU(0.2)
+    return P.act == 2 ? tanhf(v) : v;                                 // final tanh
+}
+
+__global__ void __launch_bounds__(256) pm_conv(PmConvArgs P) {
+    constexpr int TM = 64, TN = 64, TK = 16;
+    __shared__ float As[TK][TM + 4];
+    __shared__ float Bs[TK][TN + 4];
+    const int tid = threadIdx.x;
+    const int ks = P.ksplit > 1 ? P.ksplit : 1;
+    const int cls = blockIdx.z / ks, slice = blockIdx.z - cls * ks;
+    const int py = cls >> 1, px = cls & 1;
+    const int nty = P.mode == 1 ? (py == 0 ? 2 : 1) : 3;
+    const int ntx = P.mode == 1 ? (px == 0 ? 2 : 1) : 3;
+    const int Hq = P.mode == 1 ? (P.Ho - py + 1) / 2 : P.Ho;   // output rows of this class
+    const int Wq = P.mode == 1 ? (P.Wo - px + 1) / 2 : P.Wo;
+    const int N = P.B * Hq * Wq;
+    const int K = P.Cin * nty * ntx;
+    const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
+    if (n0 >= N) return;                        // (uniform: class grids are padded to the largest)
+    // this slice's K range, whole chunks
+    const int nch = (K + TK - 1) / TK, cps = (nch + ks - 1) / ks;
+    const int kbeg = slice * cps * TK, kend = min(K, (slice + 1) * cps * TK);
+    const float* __restrict__ A = P.w + P.woff[cls];
+
+    // this thread's gather column (fixed over K): n -> (window, qy, qx)
+    const int gn = tid & 63;
+    const int n = n0 + gn;
+    const bool nval = n < N;
+    int b = 0, qy = 0, qx = 0;
+    if (nval) {
+        b = n / (Hq * Wq);
+        const int r = n - b * Hq * Wq;
+        qy = r / Wq;
+        qx = r - qy * Wq;
+    }
+    const float* __restrict__ xb = P.x + (size_t)b * P.Cin * P.Hin * P.Win;
+    // the 4 A and 4 B elements this thread stages per chunk
+    auto load_a = [&](int k0, float (&ra)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = tid + 256 * j, m = m0 + (e >> 4), k = k0 + (e & 15);
+            ra[j] = (m < P.Cout && k < kend) ? A[(size_t)m * K + k] : 0.f;
+        }
+    };
+    auto load_b = [&](int k0, float (&rb)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = k0 + (tid >> 6) + 4 * j;
+            float v = 0.f;
+            if (nval && k < kend) {
+                const int ci = k / (nty * ntx);
+                const int t = k - ci * nty * ntx;
+                const int a = t / ntx, bb = t - a * ntx;
+                int iy, ix;
+                bool ok = true;
+                if (P.mode == 0) {
+                    iy = qy * P.sh + a - 1;
+                    ix = qx * P.sw + bb - 1;
+                    iy = iy < 0 ? -iy : (iy >= P.Hin ? 2 * (P.Hin - 1) - iy : iy);
+                    ix = ix < 0 ? -ix : (ix >= P.Win ? 2 * (P.Win - 1) - ix : ix);
+                } else {
+                    iy = py == 0 ? qy - a : qy;
+                    ix = px == 0 ? qx - bb : qx;
+                    ok = iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
+                }
+                if (ok) v = xb[((size_t)ci * P.Hin + iy) * P.Win + ix];
+            }
+            rb[j] = v;
+        }
+    };
+
+    const int ty = tid >> 4, tx = tid & 15;     // 4 x 4 micro-tile: rows 4ty.., cols 4tx..
+    float acc[4][4] = {};
+    float ra[4], rb[4];
+    load_a(kbeg, ra);
+    load_b(kbeg, rb);
+    for (int k0 = kbeg; k0 < kend; k0 += TK) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = tid + 256 * j;
+            As[e & 15][e >> 4] = ra[j];
+            Bs[(tid >> 6) + 4 * j][gn] = rb[j];
+        }
+        __syncthreads();
+        // next chunk's global loads in flight during this chunk's FMAs
+        if (k0 + TK < kend) {
+            load_a(k0 + TK, ra);
+            load_b(k0 + TK, rb);
+        }
+#pragma unroll
+        for (int kk = 0; kk < TK; ++kk) {
+            float a4[4], b4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a4[i] = As[kk][4 * ty + i];
+                b4[i] = Bs[kk][4 * tx + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a4[i], b4[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+    // epilogue: bias (BN folded) + activation, NCHW store -- or the raw slice partial
+    const size_t per = (size_t)P.B * P.Cout * P.Ho * P.Wo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int nn = n0 + 4 * tx + j;
+        if (nn >= N) continue;
+        const int ob = nn / (Hq * Wq);
+        const int r = nn - ob * Hq * Wq;
+        const int oqy = r / Wq, oqx = r - oqy * Wq;
+        const int oy = P.mode == 1 ? 2 * oqy + py : oqy;
+        const int ox = P.mode == 1 ? 2 * oqx + px : oqx;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int co = m0 + 4 * ty + i;
+            if (co >= P.Cout) continue;
+            const size_t o = (((size_t)ob * P.Cout + co) * P.Ho + oy) * P.Wo + ox;
+            if (ks > 1) P.part[(size_t)slice * per + o] = acc[i][j];
+            else P.y[o] = pm_act(acc[i][j] + P.bias[co], P);
+        }
+    }
+}
+
+// split-K finish: y = act(sum of the K-slice partials in slice order + bias)
+__global__ void __launch_bounds__(256) pm_reduce(PmConvArgs P) {
+    const size_t per = (size_t)P.B * P.Cout * P.Ho * P.Wo;
+    const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= per) return;
+    float s = 0.f;
+    for (int q = 0; q < P.ksplit; ++q) s += P.part[(size_t)q * per + o];
+    const int co = (int)((o / ((size_t)P.Ho * P.Wo)) % P.Cout);
+    P.y[o] = pm_act(s + P.bias[co], P);
+}
+
+}  // namespace avc

@@ -2,7 +2,8 @@
 (n_iters=1500, eps=0.1) on MI355X — BASELINE.json `metric`, configs[1] workload
 (B=256 utterances of 80x128 normalized mel per GPU, bf16 MFMA operands with fp32
 accumulation / Adam state; the fp32 path is timed too and reported beside it).
---attack e2e / fb measure configs[2] / [3] (end-to-end and feedback attacks).
+--attack e2e / fb measure configs[2] / [3] (end-to-end and feedback attacks); --attack pm
+measures configs[4] (VSMask PredictiveModel forward, windows/s of [B,1,80,100]).
 
 One "step" = one complete 1500-iteration attack over the rank's batch
 (inputs already resident in HBM).  N>1: one process per GPU (torchrun), each
@@ -45,6 +46,7 @@ FULL_CFG = {
 # FLOP per utterance-iteration (forward + input-gradient, ContentEncoder
 # hoisted out of the loop for e2e / fb)
 FLOP_PER_UTT_ITER = {"emb": 518_848_512, "e2e": 780_468_224, "fb": 1_299_316_736}
+FLOP_PER_WINDOW = 204_457_536      # PredictiveModel forward per [1,80,100] window
 PROF_ITERS = 10   # iterations of the HIP-event profiled pass (roofline)
 PEAK = {"fp32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}   # MI355X_MICROARCH.md
 
@@ -58,7 +60,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--n-iters", type=int, default=1500)
     ap.add_argument("--eps", type=float, default=0.1)
-    ap.add_argument("--attack", default="emb", choices=["emb", "e2e", "fb"])
+    ap.add_argument("--attack", default="emb", choices=["emb", "e2e", "fb", "pm"])
     ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--no-fp32-compare", action="store_true", help="skip the fp32 comparison step")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
@@ -103,8 +105,82 @@ def cpu_baseline(model, budget_s, kind="emb"):
                       f"scaled x1500; oracle/torch_cpu.py (reference ATen arithmetic incl. weight grads)"}
 
 
+def cpu_baseline_pm(budget_s, sd):
+    """Reference PredictiveModel eval forward (ATen CPU, all host threads), B=1 windows."""
+    from oracle import torch_cpu
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    x = torch.randn(1, 1, 80, 100, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        torch_cpu.pm_forward(sd, x)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            torch_cpu.pm_forward(sd, x)
+            n += 1
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(1.0 / dt, 2), "unit": "windows/s", "cores": threads, "kind": "port",
+            "sample": f"{n} B=1 forwards of a [1,1,80,100] window ({dt * 1e3:.2f} ms each); oracle/torch_cpu.pm_forward "
+                      f"(reference ATen arithmetic)"}
+
+
+def main_pm(a):
+    """configs[4]: PredictiveModel forward over B windows per GPU (step = one batched forward)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    import predictive_model
+    import shard
+    torch.manual_seed(0)
+    m = predictive_model.PredictiveModel().eval()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    md = m.to(dev)
+    B = a.batch
+    total = B * world
+    x_all = torch.randn(total, 1, 80, 100, generator=torch.Generator().manual_seed(1))
+    x = x_all[shard.shard_slice(total, rank, world)].contiguous().to(dev)
+    steps = max(a.steps, 20)                 # a step is ~ms: time at least 20 of them
+    for _ in range(max(a.warmup, 3)):
+        md(x)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        y = md(x)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    assert torch.isfinite(y).all()
+    cpu = cpu_baseline_pm(min(a.cpu_seconds, 10.0), sd) if rank == 0 and world == 1 and not a.no_cpu_baseline else None
+    if rank == 0:
+        value = total * steps / elapsed
+        achieved = FLOP_PER_WINDOW * value / world / 1e12
+        print(json.dumps({
+            "metric": "PredictiveModel windows/sec ([B,1,80,100] eval forward); 1/2/4/8 MI355X", "value": round(value, 1),
+            "unit": "windows/s", "n_gpus": world, "steps": steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"PredictiveModel forward B={B}/GPU (BASELINE configs[4]; random init seed 0)",
+                       "batch_per_gpu": B, "parallelism": f"dp{world} (independent window shards, no collective)"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK["fp32"][0], "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK["fp32"][0], 4), "traffic": None,
+                         "kernel": "pm_conv (whole forward, 12 launches)"},
+            "cpu_baseline": cpu, "flop_per_window": FLOP_PER_WINDOW}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.attack == "pm":
+        return main_pm(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

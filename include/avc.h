@@ -12,6 +12,7 @@
  *   avc_fb_attack    replaces  attack_utils.fb_attack    (/root/reference/attack_utils.py:89-130)
  *   avc_inference    replaces  AdaInVC.inference         (/root/reference/models.py:472-489)
  *   avc_attach_vc    replaces  load_state_dict of content_encoder / decoder (models.py:121-208, 346-435)
+ *   avc_pm_forward   replaces  PredictiveModel.forward   (/root/reference/models/predictive_model.py:87-110)
  *
  * The reference has no native code and no FFI of its own; the Python binding a
  * maintainer would add is shown in INTEGRATION.md (ctypes).
@@ -137,6 +138,18 @@ int avc_e2e_attack(avc_ctx* ctx, const float* vc_src, const float* vc_tgt, const
 int avc_fb_attack(avc_ctx* ctx, const float* vc_src, const float* vc_tgt, const float* adv_tgt,
                   const float* ptb0, int B, int T, float eps, int n_iters, float* out_adv,
                   const avc_attack_opts* opts, void* stream);
+
+/* ---- VSMask PredictiveModel forward (models/predictive_model.py:53-110, BASELINE config 5) ----
+ * Eval-mode inference (BatchNorm running statistics).  `weights` = HOST fp32 floating
+ * tensors of PredictiveModel.state_dict() in order (num_batches_tracked excluded). */
+typedef struct avc_pm avc_pm;
+size_t avc_pm_weight_count(void);
+int avc_pm_create(int device, const float* weights, size_t n_weights, avc_pm** out);
+void avc_pm_destroy(avc_pm* pm);
+/* output window size for an H x W input ([B,1,80,100] -> [B,1,95,63]); non-zero if too small */
+int avc_pm_out_shape(int H, int W, int* Ho, int* Wo);
+/* y[B,1,Ho,Wo] = PredictiveModel(x[B,1,H,W]); device pointers, enqueued on `stream` */
+int avc_pm_forward(avc_pm* pm, const float* x, int B, int H, int W, float* y, void* stream);
 
 /* Compute engine of a context.
  *  AUTO    (default): FUSED when the config and T allow it, else LAYERED.

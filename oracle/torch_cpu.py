@@ -143,3 +143,17 @@ def vc_attack(kind, sd, cfg, vc_src, vc_tgt, adv_tgt, eps, n_iters, ptb0, iter_h
         if iter_hook is not None:
             iter_hook(it)
     return (vc_tgt + eps * ptb.tanh()).detach()
+
+
+def pm_forward(sd, x):
+    """PredictiveModel.forward (models/predictive_model.py:87-110), eval mode, functional ATen."""
+    for i, s in enumerate([(1, 2), (2, 2), (2, 2), (2, 2), (2, 2), (2, 2), (2, 2)]):
+        p = f"down_blocks.{i}.conv."
+        x = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), sd[p + "1.weight"], sd[p + "1.bias"], stride=s)
+        x = F.batch_norm(x, sd[p + "2.running_mean"], sd[p + "2.running_var"], sd[p + "2.weight"], sd[p + "2.bias"],
+                         training=False, eps=1e-5)
+        x = F.prelu(x, sd[p + "3.weight"])
+    for i in range(5):
+        p = f"up_blocks.{i}.conv_transpose.0."
+        x = F.leaky_relu(F.conv_transpose2d(x, sd[p + "weight"], sd[p + "bias"], stride=2), 0.2)
+    return torch.tanh(x)

@@ -168,3 +168,39 @@ def test_torch_cpu_vc_baseline_matches_reference(golden, kind):
     out = torch_cpu.vc_attack(kind, sd, cfg_of(z), torch.from_numpy(z["vc_src"][:1]), torch.from_numpy(z["vc_tgt"][:1]),
                               torch.from_numpy(z["adv_tgt"][:1]), 0.1, 10, torch.from_numpy(z[f"{kind}_ptb0"][:1]))
     check_adv(out.numpy(), z[f"{kind}_adv_n10"][:1], 10)
+
+
+def test_predictive_model_oracle_and_init(golden):
+    """PredictiveModel (models/predictive_model.py:53-110): our module tree draws the
+    reference's seeded init (hashes), and the numpy oracle reproduces the reference's eval
+    forward on both window shapes of tests/golden/predictive.npz."""
+    import predictive_model
+    from oracle import predictive
+    z = golden("predictive")
+    torch.manual_seed(0)
+    m = predictive_model.PredictiveModel()
+    hs = json.loads(str(z["init_sha256"]))
+    sd = m.state_dict()
+    for k, h in hs.items():
+        assert hashlib.sha256(sd[k].numpy().tobytes()).hexdigest() == h, k
+    sdn = {k: v.numpy() for k, v in sd.items()}
+    sdn.update({k[2:]: z[k] for k in z if k.startswith("p/")})
+    for xk, yk in (("x", "y"), ("x_odd", "y_odd")):
+        out = predictive.forward(sdn, z[xk])
+        assert out.shape == z[yk].shape
+        assert rel(out, z[yk]) <= 1e-5, rel(out, z[yk])
+
+
+def test_torch_cpu_pm_baseline_matches_reference(golden):
+    """bench.py's PredictiveModel CPU baseline (oracle/torch_cpu.pm_forward) vs the reference."""
+    import predictive_model
+    from oracle import torch_cpu
+    z = golden("predictive")
+    torch.manual_seed(0)
+    sd = predictive_model.PredictiveModel().state_dict()
+    for k in z:
+        if k.startswith("p/"):
+            sd[k[2:]].copy_(torch.from_numpy(z[k]))
+    with torch.no_grad():
+        out = torch_cpu.pm_forward(sd, torch.from_numpy(z["x"]))
+    assert rel(out.numpy(), z["y"]) <= 1e-6
