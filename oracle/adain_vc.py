@@ -88,6 +88,16 @@ def relu(x):
     return np.maximum(x, 0)
 
 
+def acts(cfg):
+    """models.py:107-118 get_act: "lrelu" -> LeakyReLU(0.01), anything else ReLU.
+    Returns (act, act') with act' evaluated on the activation's output (same sign as
+    its input, which is what torch's threshold / leaky_relu backward tests)."""
+    if cfg.get("act") == "lrelu":
+        return (lambda t: np.where(t > 0, t, t * t.dtype.type(0.01)),
+                lambda y: np.where(y > 0, y.dtype.type(1), y.dtype.type(0.01)))
+    return relu, (lambda y: (y > 0).astype(y.dtype))
+
+
 def avg_pool_ceil(x, s):
     """F.avg_pool1d(kernel=s, ceil_mode=True) (models.py:206,303): the last
     window of an odd-length input averages the single remaining sample."""
@@ -144,6 +154,7 @@ class Weights:
 def se_forward(w, cfg, x, p="speaker_encoder."):
     """SpeakerEncoder.forward (models.py:327-343). Returns (emb, stash)."""
     ks = list(range(cfg["bank_scale"], cfg["bank_size"] + 1, cfg["bank_scale"]))
+    relu, _ = acts(cfg)
     st = {"x": x, "bank": []}
     outs = []
     for i, k in enumerate(ks):                                         # conv_bank 82-104
@@ -176,11 +187,12 @@ def se_forward(w, cfg, x, p="speaker_encoder."):
 
 def se_backward(w, cfg, st, g_emb, p="speaker_encoder."):
     """Input gradient d(loss)/dx of se_forward given d(loss)/d(emb)."""
+    _, d = acts(cfg)
     g = g_emb @ w(p + "output_layer.weight")
     for l in reversed(range(cfg["n_dense_blocks"])):
         y1, y2 = st["dense"][l]
-        gy2 = g * (y2 > 0)
-        gy1 = (gy2 @ w(f"{p}second_dense_layers.{l}.weight")) * (y1 > 0)
+        gy2 = g * d(y2)
+        gy1 = (gy2 @ w(f"{p}second_dense_layers.{l}.weight")) * d(y1)
         g = g + gy1 @ w(f"{p}first_dense_layers.{l}.weight")
     T_N = st["hN"].shape[2]
     gh = np.repeat((g / g.dtype.type(T_N))[:, :, None], T_N, axis=2)
@@ -188,21 +200,21 @@ def se_backward(w, cfg, st, g_emb, p="speaker_encoder."):
         s = cfg["subsample"][l]
         h, a1, a2 = st["blocks"][l]
         T = h.shape[2]
-        g2 = gh * (a2 > 0)
+        g2 = gh * d(a2)
         ga1 = pad_conv_dgrad(g2, w(f"{p}second_conv_layers.{l}.weight"), s, T)
-        g1 = ga1 * (a1 > 0)
+        g1 = ga1 * d(a1)
         gx = pad_conv_dgrad(g1, w(f"{p}first_conv_layers.{l}.weight"), 1, T)
         gres = avg_pool_ceil_backward(gh, s, T) if s > 1 else gh
         gh = gx + gres
     T = st["x"].shape[2]
-    g0 = gh * (st["h0"] > 0)
+    g0 = gh * d(st["h0"])
     Wi = w(p + "in_conv_layer.weight")
     gcat = np.einsum("oc,bot->bct", Wi[:, :, 0], g0)
     nb = len(st["bank"])
     cb = st["bank"][0].shape[1]
     gx = gcat[:, nb * cb:, :].copy()                                   # cat passthrough
     for i, o in enumerate(st["bank"]):
-        gb = gcat[:, i * cb:(i + 1) * cb, :] * (o > 0)
+        gb = gcat[:, i * cb:(i + 1) * cb, :] * d(o)
         gx += pad_conv_dgrad(gb, w(f"{p}conv_bank.{i}.weight"), 1, T)
     return gx
 
@@ -214,6 +226,7 @@ def se_backward(w, cfg, st, g_emb, p="speaker_encoder."):
 
 def ce_forward(w, cfg, x, p="content_encoder."):
     """ContentEncoder.forward -> mu (models.py:181-208; log_sigma unused by inference)."""
+    relu, _ = acts(cfg)
     ks = list(range(cfg["bank_scale"], cfg["bank_size"] + 1, cfg["bank_scale"]))
     outs = [relu(pad_conv(x, w(f"{p}conv_bank.{i}.weight"), w(f"{p}conv_bank.{i}.bias")))
             for i, _ in enumerate(ks)]
@@ -259,6 +272,7 @@ def instance_norm_backward(g, yhat, inv):
 def dec_forward(w, cfg, z, cond, p="decoder.", st=None):
     """Decoder.forward (models.py:403-435), sn=False.  st: optional list filled with
     each block's (yhat1, z1, yhat2, z2, inv1, inv2, cond1, cond2) for dec_backward."""
+    relu, _ = acts(cfg)
     out = relu(instance_norm(pad_conv(z, w(p + "in_conv_layer.weight"), w(p + "in_conv_layer.bias"))))
     for l in range(cfg["n_conv_blocks"]):
         up = cfg["upsample"][l]
@@ -278,10 +292,10 @@ def dec_forward(w, cfg, z, cond, p="decoder.", st=None):
     return pad_conv(out, w(p + "out_conv_layer.weight"), w(p + "out_conv_layer.bias"))
 
 
-def _adain_backward(g, yhat, zpre, inv, cond):
+def _adain_backward(g, yhat, zpre, inv, cond, dact):
     """act + append_cond + InstanceNorm backward: returns (d/d conv output, d/d cond)."""
     C = yhat.shape[1]
-    gz = g * (zpre > 0)
+    gz = g * dact(zpre)
     gcond = np.concatenate([gz.sum(axis=2), (gz * yhat).sum(axis=2)], axis=1)   # [mean | std]
     return instance_norm_backward(gz * cond[:, C:, None], yhat, inv), gcond
 
@@ -289,6 +303,7 @@ def _adain_backward(g, yhat, zpre, inv, cond):
 def dec_backward(w, cfg, st, g_out, p="decoder."):
     """d loss / d cond of dec_forward given d loss / d out (the content code is constant
     in the attacks, so the chain stops at the first block's AdaIN)."""
+    _, dact = acts(cfg)
     Wo = w(p + "out_conv_layer.weight")[:, :, 0]
     gh = np.einsum("oc,bot->bct", Wo, g_out)
     g_cond = np.zeros((g_out.shape[0], w(f"{p}conv_affine_layers.0.weight").shape[1]), dtype=g_out.dtype)
@@ -297,11 +312,11 @@ def dec_backward(w, cfg, st, g_out, p="decoder."):
         yh1, z1, yh2, z2, inv1, inv2, c1, c2 = st[l]
         B, C, To = gh.shape
         T = To // up
-        g2, gc2 = _adain_backward(gh, yh2, z2, inv2, c2)
+        g2, gc2 = _adain_backward(gh, yh2, z2, inv2, c2, dact)
         if up > 1:   # pixel_shuffle adjoint: pre[b, up*c + s, t] = post[b, c, up*t + s]
             g2 = g2.reshape(B, C, T, up).transpose(0, 1, 3, 2).reshape(B, C * up, T)
         ga1 = pad_conv_dgrad(g2, w(f"{p}second_conv_layers.{l}.weight"), 1, T)
-        g1, gc1 = _adain_backward(ga1, yh1, z1, inv1, c1)
+        g1, gc1 = _adain_backward(ga1, yh1, z1, inv1, c1, dact)
         g_cond += gc2 @ w(f"{p}conv_affine_layers.{2*l+1}.weight") + gc1 @ w(f"{p}conv_affine_layers.{2*l}.weight")
         ghl = gh.reshape(B, C, T, up).sum(axis=3) if up > 1 else gh     # nearest-upsample adjoint
         if l > 0:

@@ -13,10 +13,11 @@ from oracle import adain_vc as oracle
 # so element checks are only meaningful well below that.
 TOL_SE_REL = 1e-5        # SpeakerEncoder output, relative to max |emb|
 TOL_GRAD_REL = 1e-4      # d loss / d ptb at iteration 0, relative to max |grad|
-# fb chains SpeakerEncoder -> Decoder -> SpeakerEncoder: an fp32 evaluation drifts up to
-# 4.9e-4 of max |grad| from the reference's own fp32 run (a float64 restatement agrees
-# with it to 6.1e-7), from isolated elements whose ReLU masks flip between fp32 runs
-TOL_GRAD_REL_FB = 1e-3
+# e2e / fb chain through the Decoder (fb: SpeakerEncoder -> Decoder -> SpeakerEncoder):
+# an fp32 evaluation drifts up to 4.9e-4 (fb, full_T128) / 6.2e-4 (e2e, full_lrelu_T128)
+# of max |grad| from the reference's own fp32 run, while a float64 restatement agrees with
+# it to ~6e-6 -- isolated elements whose ReLU masks flip between fp32 runs
+TOL_GRAD_REL_VC = 1e-3
 # e2e / fb iteration-0 gradients vs a float64 restatement, normwise per utterance
 # (||g - g64|| / ||g64||).  The objective is ill-conditioned in fp32 at isolated inputs:
 # the numpy fp32 restatement of the reference's arithmetic itself reaches 3.4e-3 there

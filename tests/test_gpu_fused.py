@@ -127,3 +127,23 @@ def test_fused_deterministic_and_shard_invariant(full):
         hi, _, _ = ctx.emb_attack(vc[7:], at[7:], p0[7:], 0.1, 12, precision=prec)
         assert torch.equal(torch.cat([lo, hi]), a)
     ctx.set_engine("auto")
+
+
+def test_bf16_objective_after_1500(full):
+    """SURVEY.md 8(c) bf16 bound at the bench's n_iters: the final objective
+    MSE(SE(adv), SE(adv_tgt)) of the bf16 attack is within 5 % (relative) of the fp32
+    attack's, per utterance (elements of adv may differ: Adam normalises each element's
+    step, so near-zero gradients wander)."""
+    z, m, ctx = full
+    ctx.set_engine("fused")
+    g = torch.Generator().manual_seed(15)
+    vc, at, p0 = (torch.randn(4, 80, 128, generator=g).to(DEV) for _ in range(3))
+    a32, _, _ = ctx.emb_attack(vc, at, p0, 0.1, 1500)
+    a16, _, _ = ctx.emb_attack(vc, at, p0, 0.1, 1500, precision="bf16")
+    ctx.set_engine("auto")
+    tgt = ctx.se_forward(at)
+    l32 = ((ctx.se_forward(a32) - tgt) ** 2).mean(1)
+    l16 = ((ctx.se_forward(a16) - tgt) ** 2).mean(1)
+    l0 = ((ctx.se_forward(vc) - tgt) ** 2).mean(1)
+    assert (l32 < l0).all() and (l16 < l0).all()          # both attacks made progress
+    assert float(((l16 - l32).abs() / l32).max()) <= 0.05, (l16, l32)
