@@ -625,32 +625,52 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
 }
 
 // ---------------------------------------------------------------------------------
-// batched dense layer: Y[b][m] = sum_k A[m][k] X[b][k] (+ bias[m]); 64 rows x 16
-// utterances per workgroup, K in chunks of 32 staged through LDS; blockIdx.z = K slice
+// batched dense layer: Y[b][m] = sum_k A[m][k] X[b][k] (+ bias[m]); 64 rows x 32
+// utterances per workgroup, K in chunks of 32 staged through LDS with the next chunk's
+// global loads in flight during the current chunk's FMAs; blockIdx.z = K slice.  Each
+// output is one thread's k-ordered fma chain (independent of the batch).
 // ---------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) dense_batched(DenseArgs D) {
-    __shared__ float As[64][33];
-    __shared__ float Xs[16][33];
+    constexpr int TMR = 64, TB = 32, TKC = 32;
+    __shared__ float As[TKC][TMR + 1];
+    __shared__ float Xs[TKC][TB + 1];
     const int tid = threadIdx.x;
-    const int m0 = blockIdx.x * 64, b0 = blockIdx.y * 16;
+    const int m0 = blockIdx.x * TMR, b0 = blockIdx.y * TB;
     const int kb = blockIdx.z * D.kchunk, ke = min(D.K, kb + D.kchunk);
-    const int ml = tid & 63, bg = tid >> 6;         // row, utterance group of 4
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = kb; k0 < ke; k0 += 32) {
-        for (int idx = tid; idx < 64 * 32; idx += 256) {
-            const int r = idx >> 5, kk = idx & 31;
-            As[r][kk] = (m0 + r < D.M && k0 + kk < ke) ? D.A[(size_t)(m0 + r) * D.K + k0 + kk] : 0.f;
+    const int ml = tid & 63, bg = tid >> 6;         // row, utterance group of 8
+    float ra[8], rx[4];
+    auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {               // A: 64 rows x 32 k, k fastest (coalesced)
+            const int e = tid + 256 * j, r = e >> 5, kk = e & 31;
+            ra[j] = (m0 + r < D.M && k0 + kk < ke) ? D.A[(size_t)(m0 + r) * D.K + k0 + kk] : 0.f;
         }
-        for (int idx = tid; idx < 16 * 32; idx += 256) {
-            const int u = idx >> 5, kk = idx & 31;
-            Xs[u][kk] = (b0 + u < D.B && k0 + kk < ke) ? D.X[(size_t)(b0 + u) * D.K + k0 + kk] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {               // X: 32 utterances x 32 k
+            const int e = tid + 256 * j, u = e >> 5, kk = e & 31;
+            rx[j] = (b0 + u < D.B && k0 + kk < ke) ? D.X[(size_t)(b0 + u) * D.K + k0 + kk] : 0.f;
+        }
+    };
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    load(kb);
+    for (int k0 = kb; k0 < ke; k0 += TKC) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int e = tid + 256 * j;
+            As[e & 31][e >> 5] = ra[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = tid + 256 * j;
+            Xs[e & 31][e >> 5] = rx[j];
         }
         __syncthreads();
+        if (k0 + TKC < ke) load(k0 + TKC);
 #pragma unroll 8
-        for (int kk = 0; kk < 32; ++kk) {
-            const float a = As[ml][kk];
+        for (int kk = 0; kk < TKC; ++kk) {
+            const float a = As[kk][ml];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] = fmaf(a, Xs[4 * bg + u][kk], acc[u]);
+            for (int u = 0; u < 8; ++u) acc[u] = fmaf(a, Xs[kk][8 * bg + u], acc[u]);
         }
         __syncthreads();
     }
@@ -659,8 +679,8 @@ __global__ void __launch_bounds__(256) dense_batched(DenseArgs D) {
     const float bi = (D.bias && blockIdx.z == 0) ? D.bias[m] : 0.f;
     float* Y = D.Y + (size_t)blockIdx.z * D.B * D.M;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int bb = b0 + 4 * bg + u;
+    for (int u = 0; u < 8; ++u) {
+        const int bb = b0 + 8 * bg + u;
         if (bb < D.B) Y[(size_t)bb * D.M + m] = acc[u] + bi;
     }
 }
