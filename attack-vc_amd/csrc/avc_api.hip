@@ -23,6 +23,7 @@ template <int PREC, int WM, int WN, int WGM, int WGN, int KC, int MODE, int STRI
 __global__ void conv_gemm(const Problem* __restrict__ probs, int ksplit);
 __global__ void splitk_reduce(const Problem* __restrict__ probs, int ksplit);
 __global__ void se_head(HeadArgs A);
+template <bool BW>
 __global__ void se_head_v(HeadArgs A);
 __global__ void attack_init(const float* vc, const float* ptb0, float* ptb, float* m, float* v, float* adv,
                             float eps, size_t n);
@@ -162,6 +163,7 @@ struct avc_ctx {
     std::vector<DevBuf> bias_c1, bias_c2;
     DevBuf head_Wp, head_WpT, head_bias;
     DevBuf head_Wr, head_WrT;           // se_head_v: row-major dense/output weights and transposes
+    DevBuf head_Wr16, head_WrT16;       // ... as bf16 (se_head_v<true>, bf16 mode), 16-byte chunk layout
     bool fused_ok = false;              // config fits the fused per-utterance engine
     int engine = AVC_ENGINE_AUTO;       // avc_set_engine
     std::deque<DevBuf> fz_bufs;         // packed fused-engine A operands (both precisions)
@@ -583,6 +585,26 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
             }
             W.swap(o);
         };
+        // bf16 copies for the bf16 mode: chunk c (8 weights) of thread t at element
+        // ((t/64*4 + c)*64 + t%64)*8 of each matrix (one 1 KiB run per load instruction)
+        auto to16 = [&](const std::vector<float>& W, DevBuf& dst) {
+            if (c.c_h != 128 || c.c_out != 128) return;
+            std::vector<uint16_t> o(W.size());
+            for (size_t mat = 0; mat < W.size() / (128 * 128); ++mat) {
+                const float* src = W.data() + mat * 128 * 128;
+                uint16_t* d = o.data() + mat * 128 * 128;
+                for (int t = 0; t < 512; ++t)
+                    for (int cc = 0; cc < 4; ++cc)
+                        for (int i = 0; i < 8; ++i)
+                            d[((size_t)((t / 64) * 4 + cc) * 64 + (t % 64)) * 8 + i] = to_bf16(src[(size_t)t * 32 + 8 * cc + i]);
+            }
+            if (hipMalloc(&dst.p, o.size() * 2) != hipSuccess ||
+                hipMemcpy(dst.p, o.data(), o.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+                rc |= fail("avc_create: head bf16 upload failed");
+            dst.n = o.size() / 2;
+        };
+        to16(Wr, ctx->head_Wr16);
+        to16(WrT, ctx->head_WrT16);
         interleave(Wr);
         interleave(WrT);
         up(ctx->head_Wr, Wr);
@@ -666,7 +688,8 @@ extern "C" void avc_destroy(avc_ctx* ctx) {
                     &ctx->bias_c1, &ctx->bias_c2})
         for (auto& b : *v) dfree(b);
     for (DevBuf* b : {&ctx->AtF_in, &ctx->AtB_in, &ctx->AtB_bank, &ctx->bias_in, &ctx->head_Wp,
-                      &ctx->head_WpT, &ctx->head_bias, &ctx->head_Wr, &ctx->head_WrT})
+                      &ctx->head_WpT, &ctx->head_bias, &ctx->head_Wr, &ctx->head_WrT, &ctx->head_Wr16,
+                      &ctx->head_WrT16})
         dfree(*b);
     for (auto& b : ctx->fz_bufs) dfree(b);
     for (auto& kv : ctx->bf16_of) (void)hipFree(kv.second);
@@ -1089,8 +1112,11 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
         L.shmem = (size_t)(2 * c.n_dense_blocks + 5) * S * 2 * sizeof(float) +
                   (size_t)(2 * c.n_dense_blocks * c.c_h + c.c_out + 4 * c.c_out + 2) * sizeof(float);
         HeadArgs& A = L.head;
+        L.prec = prec;
         A.Wr = ctx->head_Wr.p;
         A.WrT = ctx->head_WrT.p;
+        A.Wr16 = reinterpret_cast<const uint16_t*>(ctx->head_Wr16.p);
+        A.WrT16 = reinterpret_cast<const uint16_t*>(ctx->head_WrT16.p);
         A.pooled_in = ws.pooled.p;
         A.g_pooled = attack ? ws.gpooled.p : nullptr;
         A.Wp = ctx->head_Wp.p;
@@ -1313,7 +1339,8 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
         klaunch(ev, false, se_head, L.grid, L.block, L.shmem, s, L.head);
         return hipGetLastError();
     case L_HEAD_V:
-        klaunch(ev, false, se_head_v, L.grid, L.block, L.shmem, s, L.head);
+        if (L.prec == PREC_BF16) klaunch(ev, false, se_head_v<true>, L.grid, L.block, L.shmem, s, L.head);
+        else klaunch(ev, false, se_head_v<false>, L.grid, L.block, L.shmem, s, L.head);
         return hipGetLastError();
     case L_FZ_FWD:
     case L_FZ_BWD: {

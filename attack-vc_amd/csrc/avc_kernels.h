@@ -106,6 +106,8 @@ struct HeadArgs {
     const float* Wr;          // se_head_v: row-major dense [2nd][C][C], output [D][C]
     const float* WrT;         // se_head_v: their transposes [2nd][C][C], output^T [C][D]
     int32_t tgt_parts;        // mode 3: d loss / d emb = sum of this many [B][D] slices at tgt
+    const uint16_t* Wr16;     // se_head_v<true> (bf16 mode): Wr / WrT as bf16, 16-byte chunk layout
+    const uint16_t* WrT16;
 };
 
 // ---------------------------------------------------------------------------------

@@ -7,6 +7,8 @@
 // attack_init: ptb <- ptb0, m = v = 0, adv = vc + eps*tanh(ptb) (attack_utils.py:68,78).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "avc_device.h"
 #include "avc_kernels.h"
 
@@ -315,16 +317,25 @@ __device__ __forceinline__ float quad_xor(float v) {
 struct HeadVW {
     f32x4 w[8];   // K/4 <= 32 weights of one row slice
 };
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct HeadVW16 {
+    u32x4 r[4];   // the same 32 weights as bf16 (bf16 mode), 8 per 16-byte chunk
+};
 
+// BW: bf16 weights (the bf16 mode's head; activations and accumulation stay fp32)
+template <bool BW>
 __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     // no contraction: an utterance's arithmetic must not depend on its lane in the pair
 #pragma clang fp contract(off)
+    using HW = std::conditional_t<BW, HeadVW16, HeadVW>;
     extern __shared__ float smem[];
     // every field the chain uses, hoisted out of the kernel-argument struct (lambdas that
     // capture the by-value argument by reference would spill it to scratch)
     const int C = A.C, D = A.D, nd = A.n_dense, act = A.act, Bn = A.B, mode = A.mode;
     const float* __restrict__ Wr = A.Wr;
     const float* __restrict__ WrT = A.WrT;
+    const uint16_t* __restrict__ Wr16 = A.Wr16;
+    const uint16_t* __restrict__ WrT16 = A.WrT16;
     float* __restrict__ losses = A.losses;
     const int loss_len = A.loss_len;
     const int CM = C > D ? C : D;
@@ -373,12 +384,24 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     const int NL = mode == 0 ? nf : 2 * nf;
 
     // weights of chain step i (see the table above); every step is 128 x 128
-    auto step_w = [=](int i) __attribute__((always_inline)) -> const float* {
-        if (i < 2 * nd + 1) return Wr + (size_t)i * CC;              // dense layers, then output
-        if (i == nf) return WrT + (size_t)(2 * nd) * CC;              // output^T
+    // element offset of chain step i's matrix and which set (W or W^T) holds it
+    auto step_off = [=](int i, bool& tr) __attribute__((always_inline)) -> size_t {
+        tr = i >= nf;
+        if (i < 2 * nd + 1) return (size_t)i * CC;                  // dense layers, then output
+        if (i == nf) return (size_t)(2 * nd) * CC;                  // output^T
         const int j = i - nf - 1;
         const int l = nd - 1 - j / 2;
-        return WrT + (size_t)(j % 2 == 0 ? 2 * l + 1 : 2 * l) * CC;
+        return (size_t)(j % 2 == 0 ? 2 * l + 1 : 2 * l) * CC;
+    };
+    auto step_w = [=](int i) __attribute__((always_inline)) -> const float* {
+        bool tr;
+        const size_t o = step_off(i, tr);
+        return (tr ? WrT : Wr) + o;
+    };
+    auto step_w16 = [=](int i) __attribute__((always_inline)) -> const uint16_t* {
+        bool tr;
+        const size_t o = step_off(i, tr);
+        return (tr ? WrT16 : Wr16) + o;
     };
     // C == D == 128 (fused engine): every step is a 128 x 128 matrix, K/4 = 32 weights
     // per thread -- eight unconditional 16-byte loads, no branches for the waitcnt
@@ -386,19 +409,36 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     // (host layout: chunk e of thread t at float ((t/64*8 + e)*64 + t%64)*4 of the step's
     // matrix, so every load instruction of a wave reads one contiguous 1 KiB run)
     const int wv = tid >> 6, ln = tid & 63;
-    auto load_w = [&](HeadVW& hw, int i) __attribute__((always_inline)) {
-        const float* base = step_w(i) + ((size_t)wv * 8 * 64 + ln) * 4;
+    // (bf16: chunk c of thread t at element ((t/64*4 + c)*64 + t%64)*8)
+    auto load_w = [&](HW& hw, int i) __attribute__((always_inline)) {
+        if constexpr (BW) {
+            const uint16_t* base = step_w16(i) + ((size_t)wv * 4 * 64 + ln) * 8;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+            for (int c = 0; c < 4; ++c) hw.r[c] = gload<u32x4>(reinterpret_cast<const float*>(base + (size_t)c * 64 * 8));
+        } else {
+            const float* base = step_w(i) + ((size_t)wv * 8 * 64 + ln) * 4;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
 #if AVC_HEAD_ABLATE & 1
-            hw.w[e] = f32x4{0.01f * i, 0.02f, 0.03f, 0.04f * e};
+                hw.w[e] = f32x4{0.01f * i, 0.02f, 0.03f, 0.04f * e};
 #else
-            hw.w[e] = gload<f32x4>(base + (size_t)e * 64 * 4);
+                hw.w[e] = gload<f32x4>(base + (size_t)e * 64 * 4);
 #endif
+            }
+        }
+    };
+    // weight f = 4e + j of the thread's slice (compile-time e, j)
+    auto wgt = [&](const HW& hw, int e, int j) __attribute__((always_inline)) -> float {
+        if constexpr (BW) {
+            const int f = 4 * e + j, c = f >> 3, i = f & 7;
+            const unsigned word = hw.r[c][i >> 1];
+            return __builtin_bit_cast(float, (i & 1) ? (word & 0xffff0000u) : (word << 16));
+        } else {
+            return hw.w[e][j];
         }
     };
     // out[m] (2 utterances) = sum_k W[m][k] X[k], summed over the 4 slices
-    auto dot = [&](const HeadVW& hw, int K, const f32x2* X) __attribute__((always_inline)) -> f32x2 {
+    auto dot = [&](const HW& hw, int K, const f32x2* X) __attribute__((always_inline)) -> f32x2 {
         (void)K;
         f32x2 acc = {0.f, 0.f}, acc2 = {0.f, 0.f};   // even / odd k of the pair
         const f32x4* X4 = reinterpret_cast<const f32x4*>(X);   // {X[k][0], X[k][1], X[k+1][0], X[k+1][1]}
@@ -412,10 +452,11 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
                 const f32x4 x = X4[4 * (2 * e + h) + q];
 #endif
                 // explicit fma chain: both utterance lanes round identically (shard invariance)
-                acc[0] = fmaf(hw.w[e][2 * h], x[0], acc[0]);
-                acc[1] = fmaf(hw.w[e][2 * h], x[1], acc[1]);
-                acc2[0] = fmaf(hw.w[e][2 * h + 1], x[2], acc2[0]);
-                acc2[1] = fmaf(hw.w[e][2 * h + 1], x[3], acc2[1]);
+                const float w0 = wgt(hw, e, 2 * h), w1 = wgt(hw, e, 2 * h + 1);
+                acc[0] = fmaf(w0, x[0], acc[0]);
+                acc[1] = fmaf(w0, x[1], acc[1]);
+                acc2[0] = fmaf(w1, x[2], acc2[0]);
+                acc2[1] = fmaf(w1, x[3], acc2[1]);
             }
         }
         acc[0] = acc[0] + acc2[0];
@@ -436,8 +477,9 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     // performance hint only -- any placement stays correct).
     {
         const int grp = (int)(blockIdx.x >> 3), ngrp = (int)((gridDim.x + 7) >> 3);
-        const size_t n4 = (size_t)(2 * nd + 1) * CC / 4;        // f32x4 per matrix set
-        const f32x4* W4[2] = {reinterpret_cast<const f32x4*>(Wr), reinterpret_cast<const f32x4*>(WrT)};
+        const size_t n4 = (size_t)(2 * nd + 1) * CC / (BW ? 8 : 4);        // 16-byte chunks per matrix set
+        const f32x4* W4[2] = {BW ? reinterpret_cast<const f32x4*>(Wr16) : reinterpret_cast<const f32x4*>(Wr),
+                              BW ? reinterpret_cast<const f32x4*>(WrT16) : reinterpret_cast<const f32x4*>(WrT)};
         float sink = 0.f;
         for (int t = 0; t < 2; ++t)
             for (size_t i = (size_t)grp * blockDim.x + tid; i < n4; i += (size_t)ngrp * blockDim.x) {
@@ -450,12 +492,12 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     const int step_no = mode == 0 ? 0 : *A.step;
     __syncthreads();
     // 3-step register ring (8 waves = 2 per SIMD cap a wave at 256 registers; a 4th slot spilled)
-    HeadVW w0, w1, w2;
+    HW w0, w1, w2;
     load_w(w0, 0);
     load_w(w1, min(1, NL - 1));
     load_w(w2, min(2, NL - 1));
 
-    auto run_step = [&](int i, const HeadVW& hw) __attribute__((always_inline)) {
+    auto run_step = [&](int i, const HW& hw) __attribute__((always_inline)) {
         constexpr int K = 128;
         const bool own = q == 0;
         if (i < 2 * nd) {
@@ -591,5 +633,8 @@ __global__ void attack_init(const float* __restrict__ vc, const float* __restric
     v[i] = 0.f;
     adv[i] = vc[i] + eps * tanhf(p);
 }
+
+template __global__ void se_head_v<false>(HeadArgs);
+template __global__ void se_head_v<true>(HeadArgs);
 
 }  // namespace avc
