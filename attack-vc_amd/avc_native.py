@@ -48,6 +48,14 @@ class AttackOpts(ctypes.Structure):
                 ("grad0", ctypes.c_void_p)]
 
 
+class DspCfg(ctypes.Structure):
+    _fields_ = [("sample_rate", ctypes.c_int32), ("n_fft", ctypes.c_int32), ("hop_length", ctypes.c_int32),
+                ("win_length", ctypes.c_int32), ("n_mels", ctypes.c_int32), ("preemph", ctypes.c_float),
+                ("ref_db", ctypes.c_float), ("max_db", ctypes.c_float), ("pad_mode", ctypes.c_int32)]
+
+
+PAD_MODE = {"reflect": 0, "constant": 1}
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -80,6 +88,17 @@ SIGNATURES = [
                                         ctypes.POINTER(ctypes.c_int)]),
     ("avc_pm_forward", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_dsp_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(DspCfg), ctypes.POINTER(ctypes.c_void_p)]),
+    ("avc_dsp_destroy", None, [ctypes.c_void_p]),
+    ("avc_dsp_frames", ctypes.c_int, [ctypes.POINTER(DspCfg), ctypes.c_int]),
+    ("avc_dsp_mel_basis", ctypes.c_int, [ctypes.POINTER(DspCfg), ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_dsp_wav2mel", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_dsp_mel2wav", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p]),
+    ("avc_dsp_griffin_lim", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_set_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_get_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -431,3 +450,117 @@ def predictive_forward(model: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
         hit = (version, PMContext(pm_flat_weights(model), dev))
         per[("pm", dev)] = hit
     return hit[1].forward(x)
+
+
+# --- mel front / back end (data_utils.py:16-197) ------------------------------------
+
+def dsp_cfg_struct(preprocess: Dict, pad_mode: str = "reflect") -> DspCfg:
+    """config.yaml `preprocess` section -> avc_dsp_cfg (top_db is host-side: trim)."""
+    c = DspCfg()
+    for k in ("sample_rate", "n_fft", "hop_length", "win_length", "n_mels"):
+        setattr(c, k, int(preprocess[k]))
+    for k in ("preemph", "ref_db", "max_db"):
+        setattr(c, k, float(preprocess[k]))
+    if pad_mode not in PAD_MODE:
+        raise RuntimeError(f"pad_mode must be one of {sorted(PAD_MODE)}")
+    c.pad_mode = PAD_MODE[pad_mode]
+    return c
+
+
+def mel_basis(preprocess: Dict):
+    """(librosa.filters.mel(sr, n_fft, n_mels), inv_mel_matrix) as float32 tensors, computed by
+    libavc's host code (no device needed)."""
+    c = dsp_cfg_struct(preprocess)
+    F = int(preprocess["n_fft"]) // 2 + 1
+    nm = int(preprocess["n_mels"])
+    W = torch.empty(nm, F)
+    inv = torch.empty(F, nm)
+    _check(lib().avc_dsp_mel_basis(ctypes.byref(c), ctypes.c_void_p(W.data_ptr()), ctypes.c_void_p(inv.data_ptr())))
+    return W, inv
+
+
+class Dsp:
+    """One libavc DSP context (window / twiddle / mel tables + workspace) per (config, device)."""
+
+    def __init__(self, preprocess: Dict, device: int, pad_mode: str = "reflect"):
+        self.pre = dict(preprocess)
+        self._c = dsp_cfg_struct(preprocess, pad_mode)
+        h = ctypes.c_void_p()
+        _check(lib().avc_dsp_create(int(device), ctypes.byref(self._c), ctypes.byref(h)))
+        self.h = h
+        self.device = device
+        self._lock = threading.Lock()
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.avc_dsp_destroy(h)
+
+    def frames(self, n_samples: int) -> int:
+        n = lib().avc_dsp_frames(ctypes.byref(self._c), int(n_samples))
+        if n < 0:
+            _check(1)
+        return n
+
+    @staticmethod
+    def _stats(mean, std, like):
+        if (mean is None) != (std is None):
+            raise RuntimeError("give both mean and std, or neither")
+        if mean is None:
+            return None, None
+        m = torch.as_tensor(mean, dtype=torch.float32).reshape(-1).to(like.device).contiguous()
+        s = torch.as_tensor(std, dtype=torch.float32).reshape(-1).to(like.device).contiguous()
+        return m, s
+
+    def wav2mel(self, wav: torch.Tensor, mean=None, std=None, transpose: bool = False) -> torch.Tensor:
+        """wav [B, L] (trimmed) -> mel [B, Tf, n_mels] ([B, n_mels, Tf] if transpose)."""
+        _require_gpu(wav)
+        wav = wav.contiguous()
+        if wav.dim() != 2:
+            raise RuntimeError(f"expected [B, L] waveforms, got {tuple(wav.shape)}")
+        B, L = wav.shape
+        Tf = self.frames(L)
+        nm = int(self.pre["n_mels"])
+        m, s = self._stats(mean, std, wav)
+        out = torch.empty((B, nm, Tf) if transpose else (B, Tf, nm), device=wav.device)
+        with self._lock:
+            _check(lib().avc_dsp_wav2mel(self.h, ctypes.c_void_p(wav.data_ptr()), B, L,
+                                         ctypes.c_void_p(m.data_ptr()) if m is not None else None,
+                                         ctypes.c_void_p(s.data_ptr()) if s is not None else None,
+                                         1 if transpose else 0, ctypes.c_void_p(out.data_ptr()),
+                                         ctypes.c_void_p(torch.cuda.current_stream(wav.device).cuda_stream)))
+        return out
+
+    def mel2wav(self, mel: torch.Tensor, mean=None, std=None, transpose: bool = False,
+                n_iter: int = 100) -> torch.Tensor:
+        """mel [B, Tf, n_mels] ([B, n_mels, Tf] if transpose) -> wav [B, hop * (Tf - 1)]."""
+        _require_gpu(mel)
+        mel = mel.contiguous()
+        nm = int(self.pre["n_mels"])
+        if mel.dim() != 3 or mel.shape[1 if transpose else 2] != nm:
+            raise RuntimeError(f"expected mel with {nm} bins, got {tuple(mel.shape)}")
+        B, Tf = mel.shape[0], mel.shape[2 if transpose else 1]
+        m, s = self._stats(mean, std, mel)
+        out = torch.empty(B, int(self.pre["hop_length"]) * (Tf - 1), device=mel.device)
+        with self._lock:
+            _check(lib().avc_dsp_mel2wav(self.h, ctypes.c_void_p(mel.data_ptr()), B, Tf, 1 if transpose else 0,
+                                         ctypes.c_void_p(m.data_ptr()) if m is not None else None,
+                                         ctypes.c_void_p(s.data_ptr()) if s is not None else None,
+                                         int(n_iter), ctypes.c_void_p(out.data_ptr()),
+                                         ctypes.c_void_p(torch.cuda.current_stream(mel.device).cuda_stream)))
+        return out
+
+    def griffin_lim(self, spect: torch.Tensor, n_iter: int = 100) -> torch.Tensor:
+        """spect [B, n_fft/2+1, Tf] (magnitude, the reference's layout) -> wav [B, hop * (Tf - 1)]."""
+        _require_gpu(spect)
+        spect = spect.contiguous()
+        F = int(self.pre["n_fft"]) // 2 + 1
+        if spect.dim() != 3 or spect.shape[1] != F:
+            raise RuntimeError(f"expected [B, {F}, Tf] magnitudes, got {tuple(spect.shape)}")
+        B, _, Tf = spect.shape
+        out = torch.empty(B, int(self.pre["hop_length"]) * (Tf - 1), device=spect.device)
+        with self._lock:
+            _check(lib().avc_dsp_griffin_lim(self.h, ctypes.c_void_p(spect.data_ptr()), B, Tf, int(n_iter),
+                                             ctypes.c_void_p(out.data_ptr()),
+                                             ctypes.c_void_p(torch.cuda.current_stream(spect.device).cuda_stream)))
+        return out

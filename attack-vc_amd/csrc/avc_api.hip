@@ -1698,3 +1698,4 @@ extern "C" int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len,
 
 #include "avc_vc_host.inc"
 #include "avc_pm_host.inc"
+#include "avc_dsp_host.inc"

@@ -1,0 +1,270 @@
+// Mel front / back end of the reference (data_utils.py:16-197) on gfx950:
+//   dsp_wav2mel    file2mel after load + trim (data_utils.py:99-118): pre-emphasis,
+//                  centered STFT, |X|, mel projection, dB, clip (+ normalize, 35-47)
+//   dsp_mel2mag    mel2wav's front (150-157): (denormalize,) clip, dB^-1, inv_mel_matrix
+//   dsp_gl_frames  one Griffin-Lim projection (168-197) per frame pair: STFT of the
+//                  current signal, X = S * est / max(1e-8, |est|), inverse FFT x window
+//   dsp_ola        librosa.istft's overlap-add / window-sum-square / center trim
+//   dsp_deemph     lfilter([1], [1, -preemph]) (161) as a chunked affine scan
+// STFT frames are the bandwidth unit: every frame kernel is one workgroup per PAIR of
+// real frames, packed as the real / imaginary parts of one complex N-point FFT
+// (radix-2 DIT, bit-reversed load into LDS, twiddles staged in LDS) and separated with
+// the conjugate-symmetry identities; the inverse transform of two Hermitian spectra is
+// the same FFT run on conj(X0 + i X1).  HBM traffic per Griffin-Lim iteration and frame:
+// the frame written once (N floats) and read by dsp_ola, the signal read back through L2.
+#include <hip/hip_runtime.h>
+
+#include "avc_kernels.h"
+
+namespace avc {
+
+namespace {
+constexpr int DSP_THREADS = 256;
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// in-place radix-2 DIT FFT of Z[N] (input already in bit-reversed order), forward sign
+__device__ void fft_lds(float2* Z, const float2* TW, int N, int logN) {
+    for (int s = 1; s <= logN; ++s) {
+        const int half = 1 << (s - 1), tstride = N >> s;
+        for (int j = threadIdx.x; j < (N >> 1); j += DSP_THREADS) {
+            const int k = j & (half - 1);
+            const int i0 = ((j >> (s - 1)) << s) + k, i1 = i0 + half;
+            const float2 a = Z[i0];
+            const float2 bw = cmul(Z[i1], TW[k * tstride]);
+            Z[i0] = make_float2(a.x + bw.x, a.y + bw.y);
+            Z[i1] = make_float2(a.x - bw.x, a.y - bw.y);
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ int bitrev(int n, int logN) { return (int)(__brev((unsigned)n) >> (32 - logN)); }
+
+// numpy.pad(mode='reflect') index into [0, L) (no edge repeat; any overhang), or -1 (constant)
+__device__ __forceinline__ int pad_index(int s, int L, int pad_mode) {
+    if (s >= 0 && s < L) return s;
+    if (pad_mode == 1) return -1;
+    if (L == 1) return 0;
+    const int period = 2 * (L - 1);
+    s %= period;
+    if (s < 0) s += period;
+    return s >= L ? period - s : s;
+}
+
+// X0 / X1 of the two real frames packed in Z (k in [0, N/2])
+__device__ __forceinline__ void split_pair(const float2* Z, int N, int k, float2& X0, float2& X1) {
+    const float2 a = Z[k & (N - 1)], c = Z[(N - k) & (N - 1)];
+    X0 = make_float2(0.5f * (a.x + c.x), 0.5f * (a.y - c.y));
+    X1 = make_float2(0.5f * (a.y + c.y), -0.5f * (a.x - c.x));
+}
+
+__device__ __forceinline__ void stage_twiddles(float2* TW, const float* tw, int N) {
+    for (int k = threadIdx.x; k < (N >> 1); k += DSP_THREADS)
+        TW[k] = reinterpret_cast<const float2*>(tw)[k];
+}
+}  // namespace
+
+// grid (ceil(Tf / 2), B): frames 2p, 2p + 1 of utterance b -> mel [B][Tf][n_mels] or
+// [B][n_mels][Tf] (transpose), normalized with (mean, std) when given
+__global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
+    extern __shared__ float2 dsm[];
+    const int N = A.N, F = A.F, Tf = A.Tf, L = A.L, b = blockIdx.y;
+    float2* Z = dsm;                 // [N]
+    float2* TW = Z + N;              // [N/2]
+    float* MAG = reinterpret_cast<float*>(TW + N / 2);   // [2][F]
+    stage_twiddles(TW, A.twiddle, N);
+    const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
+    const float* x = A.x + (size_t)b * L;
+    const float a = A.preemph;
+    auto sample = [&](int t, int n) -> float {
+        if (t >= Tf) return 0.f;
+        const int s = pad_index(t * A.hop + n - N / 2, L, A.pad_mode);
+        if (s < 0) return 0.f;
+        // wav = append(wav[0], wav[1:] - preemph * wav[:-1]) (data_utils.py:101)
+        return s == 0 ? x[0] : x[s] - a * x[s - 1];
+    };
+    for (int n = threadIdx.x; n < N; n += DSP_THREADS) {
+        const float w = A.window[n];
+        Z[bitrev(n, A.logN)] = make_float2(sample(t0, n) * w, sample(t1, n) * w);
+    }
+    __syncthreads();
+    fft_lds(Z, TW, N, A.logN);
+    for (int k = threadIdx.x; k < F; k += DSP_THREADS) {
+        float2 X0, X1;
+        split_pair(Z, N, k, X0, X1);
+        MAG[k] = sqrtf(X0.x * X0.x + X0.y * X0.y);
+        MAG[F + k] = sqrtf(X1.x * X1.x + X1.y * X1.y);
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 2 * A.n_mels; idx += DSP_THREADS) {
+        const int fr = idx / A.n_mels, m = idx - fr * A.n_mels, t = t0 + fr;
+        if (t >= Tf) continue;
+        const float* row = A.mel_basis + (size_t)m * F;
+        const float* mg = MAG + fr * F;
+        float s = 0.f;
+        for (int f = A.mel_range[2 * m]; f < A.mel_range[2 * m + 1]; ++f) s = fmaf(row[f], mg[f], s);
+        // 20 log10(max(1e-5, mel)); clip((mel - ref_db + max_db) / max_db, 1e-8, 1) (111-112)
+        float v = 20.f * log10f(fmaxf(1e-5f, s));
+        v = fminf(fmaxf((v - A.ref_db + A.max_db) / A.max_db, 1e-8f), 1.f);
+        if (A.mean) v = (v - A.mean[m]) / A.std[m];        // normalize (data_utils.py:35-47)
+        const size_t o = A.transpose ? ((size_t)b * A.n_mels + m) * Tf + t : ((size_t)b * Tf + t) * A.n_mels + m;
+        A.mel_out[o] = v;
+    }
+}
+
+// grid (Tf, B): spect_out[b][t][f] = sum_m inv_mel[f][m] * 10^((clip(mel, 0, 1) * max_db
+// - max_db + ref_db) * 0.05)  (data_utils.py:150-157), mel denormalized first when given
+__global__ void __launch_bounds__(DSP_THREADS) dsp_mel2mag(DspArgs A) {
+    extern __shared__ float2 dsm[];
+    float* lin = reinterpret_cast<float*>(dsm);
+    const int t = blockIdx.x, b = blockIdx.y, nm = A.n_mels, Tf = A.Tf;
+    for (int m = threadIdx.x; m < nm; m += DSP_THREADS) {
+        float v = A.mel_in[A.transpose ? ((size_t)b * nm + m) * Tf + t : ((size_t)b * Tf + t) * nm + m];
+        if (A.mean) v = v * A.std[m] + A.mean[m];          // denormalize (data_utils.py:50-62)
+        v = fminf(fmaxf(v, 0.f), 1.f) * A.max_db - A.max_db + A.ref_db;
+        lin[m] = exp10f(v * 0.05f);
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < A.F; f += DSP_THREADS) {
+        const float* r = A.inv_mel + (size_t)f * nm;
+        float s = 0.f;
+        for (int m = 0; m < nm; ++m) s = fmaf(r[m], lin[m], s);
+        A.spect_out[((size_t)b * Tf + t) * A.F + f] = s;
+    }
+}
+
+// grid (ceil(F / 256), Tf, B): [B][F][Tf] (the reference's magnitude layout) -> [B][Tf][F]
+__global__ void __launch_bounds__(DSP_THREADS) dsp_transpose(DspArgs A) {
+    const int f = blockIdx.x * DSP_THREADS + threadIdx.x, t = blockIdx.y, b = blockIdx.z;
+    if (f < A.F) A.spect_out[((size_t)b * A.Tf + t) * A.F + f] = A.spect[((size_t)b * A.F + f) * A.Tf + t];
+}
+
+// grid (ceil(Tf / 2), B): one Griffin-Lim step for frames 2p, 2p + 1 (data_utils.py:190-195):
+//   init: X = S;  else X = S * est / max(1e-8, |est|), est = STFT(y) (center, pad_mode)
+//   frames[t] = window * irfft(X[:, t])
+__global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
+    extern __shared__ float2 dsm[];
+    const int N = A.N, F = A.F, Tf = A.Tf, b = blockIdx.y, logN = A.logN;
+    float2* Z = dsm;                 // [N]
+    float2* TW = Z + N;              // [N/2]
+    float2* XB = TW + N / 2;         // [2][F]: X of both frames
+    stage_twiddles(TW, A.twiddle, N);
+    const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
+    const bool has1 = t1 < Tf;
+    const float* S0 = A.spect + ((size_t)b * Tf + t0) * F;
+    const float* S1 = has1 ? S0 + F : S0;
+    if (A.init) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < F; k += DSP_THREADS) {
+            XB[k] = make_float2(S0[k], 0.f);
+            XB[F + k] = make_float2(has1 ? S1[k] : 0.f, 0.f);
+        }
+    } else {
+        const float* y = A.y + (size_t)b * A.L;
+        for (int n = threadIdx.x; n < N; n += DSP_THREADS) {
+            const float w = A.window[n];
+            const int s0 = pad_index(t0 * A.hop + n - N / 2, A.L, A.pad_mode);
+            const int s1 = pad_index(t1 * A.hop + n - N / 2, A.L, A.pad_mode);
+            const float v0 = s0 < 0 ? 0.f : y[s0];
+            const float v1 = (!has1 || s1 < 0) ? 0.f : y[s1];
+            Z[bitrev(n, logN)] = make_float2(v0 * w, v1 * w);
+        }
+        __syncthreads();
+        fft_lds(Z, TW, N, logN);
+        for (int k = threadIdx.x; k < F; k += DSP_THREADS) {
+            float2 E0, E1;
+            split_pair(Z, N, k, E0, E1);
+            const float s0 = S0[k] / fmaxf(1e-8f, sqrtf(E0.x * E0.x + E0.y * E0.y));
+            const float s1 = has1 ? S1[k] / fmaxf(1e-8f, sqrtf(E1.x * E1.x + E1.y * E1.y)) : 0.f;
+            XB[k] = make_float2(E0.x * s0, E0.y * s0);
+            XB[F + k] = make_float2(E1.x * s1, E1.y * s1);
+        }
+    }
+    __syncthreads();
+    // conj(X0 + i X1) over the full Hermitian extension, bit-reversed; irfft ignores the
+    // imaginary parts of the DC and Nyquist bins
+    for (int k = threadIdx.x; k < N; k += DSP_THREADS) {
+        const int kk = k <= N / 2 ? k : N - k;
+        float2 X0 = XB[kk], X1 = XB[F + kk];
+        if (kk == 0 || kk == N / 2) X0.y = X1.y = 0.f;
+        if (k > N / 2) {
+            X0.y = -X0.y;
+            X1.y = -X1.y;
+        }
+        // Z = X0 + i X1 = (X0.x - X1.y) + i (X0.y + X1.x); store conj(Z)
+        Z[bitrev(k, logN)] = make_float2(X0.x - X1.y, -(X0.y + X1.x));
+    }
+    __syncthreads();
+    fft_lds(Z, TW, N, logN);
+    // z = conj(FFT(conj Z)) / N: frame0 = Re z, frame1 = Im z
+    const float invN = 1.f / (float)N;
+    float* f0 = A.frames + ((size_t)b * Tf + t0) * N;
+    for (int n = threadIdx.x; n < N; n += DSP_THREADS) {
+        const float w = A.window[n] * invN;
+        f0[n] = Z[n].x * w;
+        if (has1) f0[N + n] = -Z[n].y * w;
+    }
+}
+
+// grid (ceil(Ly / 256), B): y[j] = sum_t frames[t][s - t*hop] / wss[s], s = j + N/2
+// (librosa.istft, center=True, length=None: Ly = hop * (Tf - 1))
+__global__ void __launch_bounds__(DSP_THREADS) dsp_ola(DspArgs A) {
+    const int j = blockIdx.x * DSP_THREADS + threadIdx.x, b = blockIdx.y;
+    if (j >= A.Ly) return;
+    const int N = A.N, hop = A.hop, s = j + N / 2;
+    const int tlo = s - N + 1 <= 0 ? 0 : (s - N + hop) / hop, thi = min(A.Tf - 1, s / hop);
+    const float* fr = A.frames + (size_t)b * A.Tf * N;
+    float acc = 0.f, wss = 0.f;
+    for (int t = tlo; t <= thi; ++t) {
+        const int n = s - t * hop;
+        acc += fr[(size_t)t * N + n];
+        const float w = A.window[n];
+        wss += w * w;
+    }
+    A.y[(size_t)b * A.Ly + j] = wss > 1.17549435e-38f ? acc / wss : acc;
+}
+
+// grid (B), 1024 threads: wav = lfilter([1], [1, -a], y) -- chunk recurrences from zero,
+// an inclusive scan of the chunk maps c -> E + a^len c, then the chunks again from their
+// carries
+__global__ void __launch_bounds__(1024) dsp_deemph(DspArgs A) {
+    __shared__ float Ps[1024], Es[1024];
+    const int b = blockIdx.x, tid = threadIdx.x, Ly = A.Ly;
+    const float a = A.preemph;
+    const float* y = A.y + (size_t)b * Ly;
+    float* w = A.wav + (size_t)b * Ly;
+    const int C = (Ly + 1023) / 1024;
+    const int lo = min(Ly, tid * C), hi = min(Ly, lo + C);
+    float e = 0.f, p = 1.f;
+    for (int i = lo; i < hi; ++i) {
+        e = fmaf(a, e, y[i]);
+        p *= a;
+    }
+    Ps[tid] = p;
+    Es[tid] = e;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        float pl = 1.f, el = 0.f;
+        if (tid >= off) {
+            pl = Ps[tid - off];
+            el = Es[tid - off];
+        }
+        __syncthreads();
+        if (tid >= off) {
+            // (left then this chunk): c -> E + P (el + pl c)
+            Es[tid] = fmaf(Ps[tid], el, Es[tid]);
+            Ps[tid] = Ps[tid] * pl;
+        }
+        __syncthreads();
+    }
+    float c = tid == 0 ? 0.f : Es[tid - 1];
+    for (int i = lo; i < hi; ++i) {
+        c = fmaf(a, c, y[i]);
+        w[i] = c;
+    }
+}
+
+}  // namespace avc

@@ -243,4 +243,32 @@ struct PmConvArgs {
     float* part;                      //      partial sums to part[slice][B*Cout*Ho*Wo]; pm_reduce finishes
 };
 
+// Mel front / back end (avc_dsp.hip; data_utils.py:16-197).  One workgroup per pair of
+// STFT frames: the two real frames are the real and imaginary parts of ONE complex
+// n_fft-point FFT in LDS (radix-2, bit-reversed load, twiddles staged in LDS).
+struct DspArgs {
+    int32_t B, N, logN, F, hop, Tf;    // F = N/2 + 1 bins, Tf frames per utterance
+    int32_t L;                         // samples per utterance of the signal framed (x)
+    int32_t Ly;                        // samples per utterance of the OLA output (y)
+    int32_t n_mels, pad_mode;          // pad_mode 0: reflect (librosa 0.8 default), 1: constant
+    int32_t init;                      // dsp_gl_frames: 1 = X = spect (zero phase), 0 = project
+    int32_t transpose;                 // mel layout: 0 [B][Tf][n_mels], 1 [B][n_mels][Tf]
+    float preemph, ref_db, max_db;
+    const float* window;               // [N] periodic Hann(win_length) zero-padded to N
+    const float* twiddle;              // [N/2][2]: exp(-2 pi i k / N)
+    const float* x;                    // framed signal [B][L]
+    const float* mel_basis;            // [n_mels][F]
+    const int32_t* mel_range;          // [n_mels][2]: non-zero bins [lo, hi) of each filter
+    const float* inv_mel;              // [F][n_mels]: inv_mel_matrix (data_utils.py:16-32)
+    const float* mean;                 // [n_mels] normalize / denormalize statistics, or null
+    const float* std;
+    const float* mel_in;               // dsp_mel2mag input
+    float* mel_out;                    // dsp_wav2mel output
+    const float* spect;                // [B][Tf][F] target magnitude (Griffin-Lim)
+    float* spect_out;                  // dsp_mel2mag / dsp_transpose output
+    float* frames;                     // [B][Tf][N] windowed inverse-FFT frames
+    float* y;                          // [B][Ly] overlap-added signal
+    float* wav;                        // [B][Ly] de-emphasised output
+};
+
 }  // namespace avc

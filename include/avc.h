@@ -13,6 +13,10 @@
  *   avc_inference    replaces  AdaInVC.inference         (/root/reference/models.py:472-489)
  *   avc_attach_vc    replaces  load_state_dict of content_encoder / decoder (models.py:121-208, 346-435)
  *   avc_pm_forward   replaces  PredictiveModel.forward   (/root/reference/models/predictive_model.py:87-110)
+ *   avc_dsp_wav2mel  replaces  data_utils.file2mel after load/trim (+ normalize) (/root/reference/data_utils.py:65-118, 35-47)
+ *   avc_dsp_mel2wav  replaces  data_utils.mel2wav (+ denormalize)   (/root/reference/data_utils.py:121-165, 50-62)
+ *   avc_dsp_griffin_lim replaces data_utils.griffin_lim            (/root/reference/data_utils.py:168-197)
+ *   avc_dsp_mel_basis   replaces librosa.filters.mel / data_utils.inv_mel_matrix (data_utils.py:16-32, 110)
  *
  * The reference has no native code and no FFI of its own; the Python binding a
  * maintainer would add is shown in INTEGRATION.md (ctypes).
@@ -150,6 +154,38 @@ void avc_pm_destroy(avc_pm* pm);
 int avc_pm_out_shape(int H, int W, int* Ho, int* Wo);
 /* y[B,1,Ho,Wo] = PredictiveModel(x[B,1,H,W]); device pointers, enqueued on `stream` */
 int avc_pm_forward(avc_pm* pm, const float* x, int B, int H, int W, float* y, void* stream);
+
+/* ---- Mel front / back end (data_utils.py:16-197) ----
+ * The reference's preprocess section of config.yaml.  librosa (<= 0.9, the version the
+ * reference's positional calls need) semantics: centered frames, periodic Hann(win_length)
+ * zero-padded to n_fft, Slaney mel filters with Slaney area normalisation.  pad_mode 0 =
+ * reflect (librosa 0.8 stft default), 1 = constant.  n_fft: power of two in [16, 4096]. */
+typedef struct {
+    int32_t sample_rate, n_fft, hop_length, win_length, n_mels;
+    float preemph, ref_db, max_db;
+    int32_t pad_mode;
+} avc_dsp_cfg;
+typedef struct avc_dsp avc_dsp;
+int avc_dsp_create(int device, const avc_dsp_cfg* cfg, avc_dsp** out);
+void avc_dsp_destroy(avc_dsp* dsp);
+/* STFT frames of an n-sample signal: 1 + n / hop_length (-1 on a bad config) */
+int avc_dsp_frames(const avc_dsp_cfg* cfg, int n_samples);
+/* HOST outputs (no device needed): mel_basis [n_mels][n_fft/2+1] = librosa.filters.mel(sr,
+ * n_fft, n_mels); inv_mel [n_fft/2+1][n_mels] = inv_mel_matrix (either may be NULL) */
+int avc_dsp_mel_basis(const avc_dsp_cfg* cfg, float* mel_basis, float* inv_mel);
+/* file2mel after load + trim: wav [B][L] (trimmed waveforms of equal length L) ->
+ * mel [B][Tf][n_mels] (transpose 0, file2mel's layout) or [B][n_mels][Tf] (transpose 1, the
+ * attacks' [B,80,T] input), Tf = avc_dsp_frames(L).  mean / std (device [n_mels], both or
+ * neither) fold normalize() in. */
+int avc_dsp_wav2mel(avc_dsp* dsp, const float* wav, int B, int L, const float* mean, const float* std,
+                    int transpose, float* mel, void* stream);
+/* mel2wav: mel in the same layouts (denormalize() folded in when mean / std are given) ->
+ * wav [B][hop_length * (Tf - 1)]: inverse dB, inv_mel_matrix, n_iter Griffin-Lim
+ * iterations (the reference uses 100), de-emphasis. */
+int avc_dsp_mel2wav(avc_dsp* dsp, const float* mel, int B, int Tf, int transpose, const float* mean,
+                    const float* std, int n_iter, float* wav, void* stream);
+/* griffin_lim(spect [B][n_fft/2+1][Tf], hop, win, n_fft, n_iter) -> wav [B][hop_length * (Tf - 1)] */
+int avc_dsp_griffin_lim(avc_dsp* dsp, const float* spect, int B, int Tf, int n_iter, float* wav, void* stream);
 
 /* Compute engine of a context.
  *  AUTO    (default): FUSED when the config and T allow it, else LAYERED.
