@@ -99,6 +99,10 @@ SIGNATURES = [
                                        ctypes.c_void_p]),
     ("avc_dsp_griffin_lim", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_dsp_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("avc_dsp_profile_count", ctypes.c_int, [ctypes.c_void_p]),
+    ("avc_dsp_profile_kernel", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double)]),
     ("avc_set_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_get_engine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -563,4 +567,17 @@ class Dsp:
             _check(lib().avc_dsp_griffin_lim(self.h, ctypes.c_void_p(spect.data_ptr()), B, Tf, int(n_iter),
                                              ctypes.c_void_p(out.data_ptr()),
                                              ctypes.c_void_p(torch.cuda.current_stream(spect.device).cuda_stream)))
+        return out
+
+    def set_profiling(self, on: bool):
+        _check(lib().avc_dsp_set_profiling(self.h, 1 if on else 0))
+
+    def profile(self) -> Dict[str, Tuple[int, float]]:
+        """{kernel name: (launches, total device ms)} since set_profiling(True)."""
+        out = {}
+        for i in range(lib().avc_dsp_profile_count(self.h)):
+            name = ctypes.create_string_buffer(128)
+            n, ms = ctypes.c_long(), ctypes.c_double()
+            _check(lib().avc_dsp_profile_kernel(self.h, i, name, 128, ctypes.byref(n), ctypes.byref(ms)))
+            out[name.value.decode()] = (n.value, ms.value)
         return out

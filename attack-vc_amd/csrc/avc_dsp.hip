@@ -8,7 +8,7 @@
 //   dsp_deemph     lfilter([1], [1, -preemph]) (161) as a chunked affine scan
 // STFT frames are the bandwidth unit: every frame kernel is one workgroup per PAIR of
 // real frames, packed as the real / imaginary parts of one complex N-point FFT
-// (radix-2 DIT, bit-reversed load into LDS, twiddles staged in LDS) and separated with
+// (radix-4 DIT passes, bit-reversed load into LDS, twiddles staged in LDS) and separated with
 // the conjugate-symmetry identities; the inverse transform of two Hermitian spectra is
 // the same FFT run on conj(X0 + i X1).  HBM traffic per Griffin-Lim iteration and frame:
 // the frame written once (N floats) and read by dsp_ola, the signal read back through L2.
@@ -25,9 +25,32 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
-// in-place radix-2 DIT FFT of Z[N] (input already in bit-reversed order), forward sign
+// in-place DIT FFT of Z[N] (input already in bit-reversed order), forward sign: pairs of
+// radix-2 stages fused into one radix-4 pass (4 LDS reads / writes per 4 butterflies, one
+// barrier per pass), a final radix-2 pass when log2 N is odd
 __device__ void fft_lds(float2* Z, const float2* TW, int N, int logN) {
-    for (int s = 1; s <= logN; ++s) {
+    int s = 1;
+    for (; s + 1 <= logN; s += 2) {
+        const int half = 1 << (s - 1), t1 = N >> s, t2 = N >> (s + 1);
+        for (int j = threadIdx.x; j < (N >> 2); j += DSP_THREADS) {
+            const int k = j & (half - 1);
+            const int i0 = ((j >> (s - 1)) << (s + 1)) + k;
+            float2 a = Z[i0], b = Z[i0 + half], c = Z[i0 + 2 * half], d = Z[i0 + 3 * half];
+            // stage s: (a, b), (c, d) with W_{2 half}^k
+            const float2 w1 = TW[k * t1];
+            const float2 bw = cmul(b, w1), dw = cmul(d, w1);
+            const float2 a1 = make_float2(a.x + bw.x, a.y + bw.y), b1 = make_float2(a.x - bw.x, a.y - bw.y);
+            const float2 c1 = make_float2(c.x + dw.x, c.y + dw.y), d1 = make_float2(c.x - dw.x, c.y - dw.y);
+            // stage s + 1: (a1, c1) with W_{4 half}^k, (b1, d1) with W_{4 half}^{k + half}
+            const float2 cw = cmul(c1, TW[k * t2]), dw2 = cmul(d1, TW[(k + half) * t2]);
+            Z[i0] = make_float2(a1.x + cw.x, a1.y + cw.y);
+            Z[i0 + 2 * half] = make_float2(a1.x - cw.x, a1.y - cw.y);
+            Z[i0 + half] = make_float2(b1.x + dw2.x, b1.y + dw2.y);
+            Z[i0 + 3 * half] = make_float2(b1.x - dw2.x, b1.y - dw2.y);
+        }
+        __syncthreads();
+    }
+    if (s == logN) {
         const int half = 1 << (s - 1), tstride = N >> s;
         for (int j = threadIdx.x; j < (N >> 1); j += DSP_THREADS) {
             const int k = j & (half - 1);
@@ -129,9 +152,9 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_mel2mag(DspArgs A) {
     }
     __syncthreads();
     for (int f = threadIdx.x; f < A.F; f += DSP_THREADS) {
-        const float* r = A.inv_mel + (size_t)f * nm;
+        // inv_mel stored transposed [n_mels][F]: consecutive threads read consecutive bins
         float s = 0.f;
-        for (int m = 0; m < nm; ++m) s = fmaf(r[m], lin[m], s);
+        for (int m = 0; m < nm; ++m) s = fmaf(A.inv_mel[(size_t)m * A.F + f], lin[m], s);
         A.spect_out[((size_t)b * Tf + t) * A.F + f] = s;
     }
 }

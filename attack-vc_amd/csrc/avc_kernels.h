@@ -259,7 +259,7 @@ struct DspArgs {
     const float* x;                    // framed signal [B][L]
     const float* mel_basis;            // [n_mels][F]
     const int32_t* mel_range;          // [n_mels][2]: non-zero bins [lo, hi) of each filter
-    const float* inv_mel;              // [F][n_mels]: inv_mel_matrix (data_utils.py:16-32)
+    const float* inv_mel;              // [n_mels][F]: inv_mel_matrix^T (data_utils.py:16-32)
     const float* mean;                 // [n_mels] normalize / denormalize statistics, or null
     const float* std;
     const float* mel_in;               // dsp_mel2mag input

@@ -3,7 +3,10 @@
 (B=256 utterances of 80x128 normalized mel per GPU, bf16 MFMA operands with fp32
 accumulation / Adam state; the fp32 path is timed too and reported beside it).
 --attack e2e / fb measure configs[2] / [3] (end-to-end and feedback attacks); --attack pm
-measures configs[4] (VSMask PredictiveModel forward, windows/s of [B,1,80,100]).
+measures configs[4] (VSMask PredictiveModel forward, windows/s of [B,1,80,100]);
+--attack mel2wav measures the back end after the attack: denormalize +
+mel2wav (inverse dB, inv_mel_matrix, 100 Griffin-Lim iterations, de-emphasis) of B defended
+80x128 mels per GPU, vocoded utts/s.
 
 One "step" = one complete 1500-iteration attack over the rank's batch
 (inputs already resident in HBM).  N>1: one process per GPU (torchrun), each
@@ -47,6 +50,11 @@ FULL_CFG = {
 # hoisted out of the loop for e2e / fb)
 FLOP_PER_UTT_ITER = {"emb": 518_848_512, "e2e": 780_468_224, "fb": 1_299_316_736}
 FLOP_PER_WINDOW = 204_457_536      # PredictiveModel forward per [1,80,100] window
+# assumed AdaIN-VC config.yaml `preprocess` section (not in the container)
+PREPROCESS = dict(sample_rate=16000, preemph=0.97, n_fft=2048, hop_length=300, win_length=1200, n_mels=80,
+                  ref_db=20, max_db=100, top_db=15)
+GL_ITERS = 100    # data_utils.py:172 (griffin_lim n_iter default)
+HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
 PROF_ITERS = 10   # iterations of the HIP-event profiled pass (roofline)
 PEAK = {"fp32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}   # MI355X_MICROARCH.md
 
@@ -60,7 +68,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--n-iters", type=int, default=1500)
     ap.add_argument("--eps", type=float, default=0.1)
-    ap.add_argument("--attack", default="emb", choices=["emb", "e2e", "fb", "pm"])
+    ap.add_argument("--attack", default="emb", choices=["emb", "e2e", "fb", "pm", "mel2wav"])
     ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--no-fp32-compare", action="store_true", help="skip the fp32 comparison step")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
@@ -177,10 +185,115 @@ def main_pm(a):
         dist.destroy_process_group()
 
 
+def cpu_baseline_mel2wav(budget_s, mel):
+    """The reference's mel2wav (numpy float64 restatement of data_utils.py:121-197 with
+    librosa 0.8 semantics, oracle/mel_dsp.py) on one utterance, host threads as numpy uses them."""
+    from oracle import mel_dsp
+    pre = {k: v for k, v in PREPROCESS.items() if k != "top_db"}
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        mel_dsp.mel2wav(mel, **pre, n_iter=GL_ITERS)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(1.0 / dt, 4), "unit": "utts/s", "cores": 1, "kind": "port",
+            "sample": f"{n} single-utterance mel2wav calls (80x{mel.shape[0]} mel, {GL_ITERS} Griffin-Lim iterations, "
+                      f"{dt:.2f} s each); oracle/mel_dsp.py (numpy pocketfft, float64, one thread)"}
+
+
+def main_mel2wav(a):
+    """Back end: B defended mels per GPU -> waveforms (step = one batched mel2wav)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    import data_utils
+    import shard
+    B, T = a.batch, a.frames
+    total = B * world
+    g = torch.Generator().manual_seed(1)
+    # normalized mels ~ N(0,1) (data_utils.py:35-47) with per-bin statistics of a dB-scaled
+    # spectrogram in [0, 1]
+    mean = torch.linspace(0.35, 0.55, 80, dtype=torch.float64)
+    std = torch.linspace(0.12, 0.2, 80, dtype=torch.float64)
+    mel_all = torch.randn(total, 80, T, generator=g)
+    mel = mel_all[shard.shard_slice(total, rank, world)].contiguous().to(dev)
+    attr = {"mean": mean.numpy(), "std": std.numpy()}
+    d = data_utils.dsp_for(PREPROCESS, dev)
+
+    def step():
+        return d.mel2wav(mel, attr["mean"], attr["std"], True, GL_ITERS)
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    assert torch.isfinite(out).all()
+    roof = None
+    if not a.no_roofline:
+        d.set_profiling(True)
+        step()
+        stats = d.profile()
+        d.set_profiling(False)
+        N, hop = PREPROCESS["n_fft"], PREPROCESS["hop_length"]
+        F = N // 2 + 1
+        Tf = T
+        # algorithmic HBM bytes per frame: dsp_gl_frames reads the target magnitude (F) and
+        # the signal's new samples (hop), writes the windowed frame (N); dsp_ola reads the
+        # frames (N) and writes the signal (hop)
+        per_frame = {"dsp_gl_frames": (F + hop + N) * 4, "dsp_ola": (N + hop) * 4}
+        name = "dsp_gl_frames"
+        n, ms = stats[name]
+        avg = ms / n
+        achieved = per_frame[name] * B * Tf / (avg * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK, 4), "traffic": None, "kernel": name,
+                "avg_launch_ms": round(avg, 4), "bytes_per_launch": per_frame[name] * B * Tf,
+                "per_kernel": {k: {"launches": v[0], "avg_ms": round(v[1] / v[0], 4)} for k, v in stats.items()}}
+        tpath = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tpath):
+            tr = json.load(open(tpath)).get("mel2wav", {}).get(name)
+            if tr is not None:
+                roof["traffic"] = tr
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        import numpy as np
+        m0 = (mel[0].T.double().cpu().numpy() * attr["std"] + attr["mean"]).astype(np.float32)
+        cpu = cpu_baseline_mel2wav(min(a.cpu_seconds, 20.0), m0)
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"vocoded utts/sec (denormalize + mel2wav, {GL_ITERS} Griffin-Lim iterations, 80x{T} mel); "
+                      "1/2/4/8 MI355X", "value": round(total * a.steps / elapsed, 2), "unit": "utts/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"mel2wav B={B}/GPU, 80x{T} normalized mels, preprocess {PREPROCESS} "
+                                   f"(assumed AdaIN-VC config)", "batch_per_gpu": B, "frames": T,
+                       "parallelism": f"dp{world} (independent utterance shards, no collective)"},
+            "roofline": roof, "cpu_baseline": cpu}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     if a.attack == "pm":
         return main_pm(a)
+    if a.attack == "mel2wav":
+        return main_mel2wav(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

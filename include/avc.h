@@ -186,6 +186,12 @@ int avc_dsp_mel2wav(avc_dsp* dsp, const float* mel, int B, int Tf, int transpose
                     const float* std, int n_iter, float* wav, void* stream);
 /* griffin_lim(spect [B][n_fft/2+1][Tf], hop, win, n_fft, n_iter) -> wav [B][hop_length * (Tf - 1)] */
 int avc_dsp_griffin_lim(avc_dsp* dsp, const float* spect, int B, int Tf, int n_iter, float* wav, void* stream);
+/* Per-launch HIP-event profiling of a DSP context (bench.py's roofline): while enabled every
+ * launch is bracketed by events on the call's stream (and synchronised); per kernel name the
+ * launch count and device milliseconds accumulate.  Enabling clears the counters. */
+int avc_dsp_set_profiling(avc_dsp* dsp, int enable);
+int avc_dsp_profile_count(avc_dsp* dsp);
+int avc_dsp_profile_kernel(avc_dsp* dsp, int i, char* name, int name_len, long* launches, double* total_ms);
 
 /* Compute engine of a context.
  *  AUTO    (default): FUSED when the config and T allow it, else LAYERED.
