@@ -21,6 +21,11 @@ namespace avc {
 namespace {
 constexpr int DSP_THREADS = 256;
 
+// LDS slot of complex element i: one float2 of padding per 32 (bit-reversed stores and the
+// early radix-4 passes would otherwise hit one bank set 64- / 8-way)
+__device__ __forceinline__ int zp(int i) { return i + (i >> 5); }
+__host__ __device__ constexpr int zlen(int N) { return N + N / 32; }
+
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -35,7 +40,7 @@ __device__ void fft_lds(float2* Z, const float2* TW, int N, int logN) {
         for (int j = threadIdx.x; j < (N >> 2); j += DSP_THREADS) {
             const int k = j & (half - 1);
             const int i0 = ((j >> (s - 1)) << (s + 1)) + k;
-            float2 a = Z[i0], b = Z[i0 + half], c = Z[i0 + 2 * half], d = Z[i0 + 3 * half];
+            float2 a = Z[zp(i0)], b = Z[zp(i0 + half)], c = Z[zp(i0 + 2 * half)], d = Z[zp(i0 + 3 * half)];
             // stage s: (a, b), (c, d) with W_{2 half}^k
             const float2 w1 = TW[k * t1];
             const float2 bw = cmul(b, w1), dw = cmul(d, w1);
@@ -43,10 +48,10 @@ __device__ void fft_lds(float2* Z, const float2* TW, int N, int logN) {
             const float2 c1 = make_float2(c.x + dw.x, c.y + dw.y), d1 = make_float2(c.x - dw.x, c.y - dw.y);
             // stage s + 1: (a1, c1) with W_{4 half}^k, (b1, d1) with W_{4 half}^{k + half}
             const float2 cw = cmul(c1, TW[k * t2]), dw2 = cmul(d1, TW[(k + half) * t2]);
-            Z[i0] = make_float2(a1.x + cw.x, a1.y + cw.y);
-            Z[i0 + 2 * half] = make_float2(a1.x - cw.x, a1.y - cw.y);
-            Z[i0 + half] = make_float2(b1.x + dw2.x, b1.y + dw2.y);
-            Z[i0 + 3 * half] = make_float2(b1.x - dw2.x, b1.y - dw2.y);
+            Z[zp(i0)] = make_float2(a1.x + cw.x, a1.y + cw.y);
+            Z[zp(i0 + 2 * half)] = make_float2(a1.x - cw.x, a1.y - cw.y);
+            Z[zp(i0 + half)] = make_float2(b1.x + dw2.x, b1.y + dw2.y);
+            Z[zp(i0 + 3 * half)] = make_float2(b1.x - dw2.x, b1.y - dw2.y);
         }
         __syncthreads();
     }
@@ -55,10 +60,10 @@ __device__ void fft_lds(float2* Z, const float2* TW, int N, int logN) {
         for (int j = threadIdx.x; j < (N >> 1); j += DSP_THREADS) {
             const int k = j & (half - 1);
             const int i0 = ((j >> (s - 1)) << s) + k, i1 = i0 + half;
-            const float2 a = Z[i0];
-            const float2 bw = cmul(Z[i1], TW[k * tstride]);
-            Z[i0] = make_float2(a.x + bw.x, a.y + bw.y);
-            Z[i1] = make_float2(a.x - bw.x, a.y - bw.y);
+            const float2 a = Z[zp(i0)];
+            const float2 bw = cmul(Z[zp(i1)], TW[k * tstride]);
+            Z[zp(i0)] = make_float2(a.x + bw.x, a.y + bw.y);
+            Z[zp(i1)] = make_float2(a.x - bw.x, a.y - bw.y);
         }
         __syncthreads();
     }
@@ -79,7 +84,7 @@ __device__ __forceinline__ int pad_index(int s, int L, int pad_mode) {
 
 // X0 / X1 of the two real frames packed in Z (k in [0, N/2])
 __device__ __forceinline__ void split_pair(const float2* Z, int N, int k, float2& X0, float2& X1) {
-    const float2 a = Z[k & (N - 1)], c = Z[(N - k) & (N - 1)];
+    const float2 a = Z[zp(k & (N - 1))], c = Z[zp((N - k) & (N - 1))];
     X0 = make_float2(0.5f * (a.x + c.x), 0.5f * (a.y - c.y));
     X1 = make_float2(0.5f * (a.y + c.y), -0.5f * (a.x - c.x));
 }
@@ -95,8 +100,8 @@ __device__ __forceinline__ void stage_twiddles(float2* TW, const float* tw, int 
 __global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
     extern __shared__ float2 dsm[];
     const int N = A.N, F = A.F, Tf = A.Tf, L = A.L, b = blockIdx.y;
-    float2* Z = dsm;                 // [N]
-    float2* TW = Z + N;              // [N/2]
+    float2* Z = dsm;                 // [zlen(N)]
+    float2* TW = Z + zlen(N);        // [N/2]
     float* MAG = reinterpret_cast<float*>(TW + N / 2);   // [2][F]
     stage_twiddles(TW, A.twiddle, N);
     const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
@@ -111,7 +116,7 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
     };
     for (int n = threadIdx.x; n < N; n += DSP_THREADS) {
         const float w = A.window[n];
-        Z[bitrev(n, A.logN)] = make_float2(sample(t0, n) * w, sample(t1, n) * w);
+        Z[zp(bitrev(n, A.logN))] = make_float2(sample(t0, n) * w, sample(t1, n) * w);
     }
     __syncthreads();
     fft_lds(Z, TW, N, A.logN);
@@ -169,66 +174,86 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_transpose(DspArgs A) {
 //   init: X = S;  else X = S * est / max(1e-8, |est|), est = STFT(y) (center, pad_mode)
 //   frames[t] = window * irfft(X[:, t])
 __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
+    // bins per thread: k = tid + 256 i, i < KPT covers F = N/2 + 1 <= 2049 (N <= 4096);
+    // both spectra stay in registers between the forward and inverse transforms, so the
+    // LDS holds only the FFT buffer and the twiddles (more workgroups per CU)
+    constexpr int KPT = (4096 / 2 + 1 + DSP_THREADS - 1) / DSP_THREADS;
     extern __shared__ float2 dsm[];
-    const int N = A.N, F = A.F, Tf = A.Tf, b = blockIdx.y, logN = A.logN;
-    float2* Z = dsm;                 // [N]
-    float2* TW = Z + N;              // [N/2]
-    float2* XB = TW + N / 2;         // [2][F]: X of both frames
-    stage_twiddles(TW, A.twiddle, N);
+    const int N = A.N, F = A.F, Tf = A.Tf, b = blockIdx.y, logN = A.logN, tid = threadIdx.x;
+    float2* Z = dsm;                 // [zlen(N)]
+    float2* TW = Z + zlen(N);        // [N/2]
     const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
     const bool has1 = t1 < Tf;
     const float* S0 = A.spect + ((size_t)b * Tf + t0) * F;
     const float* S1 = has1 ? S0 + F : S0;
+    // target magnitudes first: their loads are in flight during the gather and forward FFT
+    float m0[KPT], m1[KPT];
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+        const int k = tid + DSP_THREADS * i;
+        m0[i] = k < F ? S0[k] : 0.f;
+        m1[i] = (k < F && has1) ? S1[k] : 0.f;
+    }
+    float2 X0[KPT], X1[KPT];
     if (A.init) {
-        __syncthreads();
-        for (int k = threadIdx.x; k < F; k += DSP_THREADS) {
-            XB[k] = make_float2(S0[k], 0.f);
-            XB[F + k] = make_float2(has1 ? S1[k] : 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
+            X0[i] = make_float2(m0[i], 0.f);
+            X1[i] = make_float2(m1[i], 0.f);
         }
+        stage_twiddles(TW, A.twiddle, N);
     } else {
         const float* y = A.y + (size_t)b * A.L;
-        for (int n = threadIdx.x; n < N; n += DSP_THREADS) {
+        for (int n = tid; n < N; n += DSP_THREADS) {
             const float w = A.window[n];
             const int s0 = pad_index(t0 * A.hop + n - N / 2, A.L, A.pad_mode);
             const int s1 = pad_index(t1 * A.hop + n - N / 2, A.L, A.pad_mode);
             const float v0 = s0 < 0 ? 0.f : y[s0];
             const float v1 = (!has1 || s1 < 0) ? 0.f : y[s1];
-            Z[bitrev(n, logN)] = make_float2(v0 * w, v1 * w);
+            Z[zp(bitrev(n, logN))] = make_float2(v0 * w, v1 * w);
         }
+        stage_twiddles(TW, A.twiddle, N);
         __syncthreads();
         fft_lds(Z, TW, N, logN);
-        for (int k = threadIdx.x; k < F; k += DSP_THREADS) {
-            float2 E0, E1;
-            split_pair(Z, N, k, E0, E1);
-            const float s0 = S0[k] / fmaxf(1e-8f, sqrtf(E0.x * E0.x + E0.y * E0.y));
-            const float s1 = has1 ? S1[k] / fmaxf(1e-8f, sqrtf(E1.x * E1.x + E1.y * E1.y)) : 0.f;
-            XB[k] = make_float2(E0.x * s0, E0.y * s0);
-            XB[F + k] = make_float2(E1.x * s1, E1.y * s1);
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
+            const int k = tid + DSP_THREADS * i;
+            X0[i] = X1[i] = make_float2(0.f, 0.f);
+            if (k < F) {
+                float2 E0, E1;
+                split_pair(Z, N, k, E0, E1);
+                const float s0 = m0[i] / fmaxf(1e-8f, sqrtf(E0.x * E0.x + E0.y * E0.y));
+                const float s1 = has1 ? m1[i] / fmaxf(1e-8f, sqrtf(E1.x * E1.x + E1.y * E1.y)) : 0.f;
+                X0[i] = make_float2(E0.x * s0, E0.y * s0);
+                X1[i] = make_float2(E1.x * s1, E1.y * s1);
+            }
         }
     }
-    __syncthreads();
-    // conj(X0 + i X1) over the full Hermitian extension, bit-reversed; irfft ignores the
-    // imaginary parts of the DC and Nyquist bins
-    for (int k = threadIdx.x; k < N; k += DSP_THREADS) {
-        const int kk = k <= N / 2 ? k : N - k;
-        float2 X0 = XB[kk], X1 = XB[F + kk];
-        if (kk == 0 || kk == N / 2) X0.y = X1.y = 0.f;
-        if (k > N / 2) {
-            X0.y = -X0.y;
-            X1.y = -X1.y;
+    __syncthreads();   // every read of the forward spectrum is done
+    // conj(X0 + i X1) over the full Hermitian extension (bins k and N - k from the same
+    // thread), bit-reversed; irfft ignores the imaginary parts of the DC and Nyquist bins
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+        const int k = tid + DSP_THREADS * i;
+        if (k < F) {
+            float2 a = X0[i], c = X1[i];
+            if (k == 0 || k == N / 2) a.y = c.y = 0.f;
+            // Z = X0 + i X1 = (X0.x - X1.y) + i (X0.y + X1.x); store conj(Z)
+            Z[zp(bitrev(k, logN))] = make_float2(a.x - c.y, -(a.y + c.x));
+            if (k != 0 && k != N / 2)   // bin N - k: conj(X0) + i conj(X1)
+                Z[zp(bitrev(N - k, logN))] = make_float2(a.x + c.y, a.y - c.x);
         }
-        // Z = X0 + i X1 = (X0.x - X1.y) + i (X0.y + X1.x); store conj(Z)
-        Z[bitrev(k, logN)] = make_float2(X0.x - X1.y, -(X0.y + X1.x));
     }
     __syncthreads();
     fft_lds(Z, TW, N, logN);
     // z = conj(FFT(conj Z)) / N: frame0 = Re z, frame1 = Im z
     const float invN = 1.f / (float)N;
     float* f0 = A.frames + ((size_t)b * Tf + t0) * N;
-    for (int n = threadIdx.x; n < N; n += DSP_THREADS) {
+    for (int n = tid; n < N; n += DSP_THREADS) {
         const float w = A.window[n] * invN;
-        f0[n] = Z[n].x * w;
-        if (has1) f0[N + n] = -Z[n].y * w;
+        const float2 z = Z[zp(n)];
+        f0[n] = z.x * w;
+        if (has1) f0[N + n] = -z.y * w;
     }
 }
 
