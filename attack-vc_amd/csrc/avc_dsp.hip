@@ -266,6 +266,9 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_ola(DspArgs A) {
     const int tlo = s - N + 1 <= 0 ? 0 : (s - N + hop) / hop, thi = min(A.Tf - 1, s / hop);
     const float* fr = A.frames + (size_t)b * A.Tf * N;
     float acc = 0.f, wss = 0.f;
+    // independent frame loads: unrolled so several are in flight per thread (the sum
+    // stays in frame order, like librosa's sequential overlap-add)
+#pragma unroll 8
     for (int t = tlo; t <= thi; ++t) {
         const int n = s - t * hop;
         acc += fr[(size_t)t * N + n];
