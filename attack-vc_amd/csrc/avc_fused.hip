@@ -702,7 +702,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     // 16-byte accesses; a batch's loads all issued before its arithmetic (one HBM round
     // trip per batch instead of one per element)
     const int n4 = FZ_CIN * T / 4;
-    constexpr int AB = 5;                       // f32x4 per thread per batch
+    constexpr int AB = 10;                      // f32x4 per thread per batch (T = 128: one batch)
     for (int q0 = 0; q0 < n4; q0 += 256 * AB) {
         f32x4 P[AB], M[AB], V[AB], X[AB];
 #pragma unroll

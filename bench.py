@@ -269,6 +269,23 @@ def main_mel2wav(a):
             tr = json.load(open(tpath)).get("mel2wav", {}).get(name)
             if tr is not None:
                 roof["traffic"] = tr
+    # front end on the same shapes: B trimmed waveforms of hop * (T - 1) samples -> normalized
+    # [B, 80, T] mels (file2mel after load / trim + normalize, one dsp_wav2mel launch)
+    wav = out.contiguous()
+    for _ in range(3):
+        d.wav2mel(wav, attr["mean"], attr["std"], True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        mel_fe = d.wav2mel(wav, attr["mean"], attr["std"], True)
+    e1.record()
+    torch.cuda.synchronize()
+    fe_ms = e0.elapsed_time(e1) / 20
+    assert mel_fe.shape == (B, 80, T) and torch.isfinite(mel_fe).all()
+    fe_bytes = B * (wav.shape[1] + 80 * T) * 4          # algorithmic: read the waveform, write the mel
+    front = {"kernel": "dsp_wav2mel", "utts_per_s": round(B / (fe_ms * 1e-3), 1), "avg_launch_ms": round(fe_ms, 4),
+             "bytes_per_launch": fe_bytes, "hbm_frac": round(fe_bytes / (fe_ms * 1e-3) / 1e9 / HBM_PEAK, 4)}
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         import numpy as np
@@ -283,7 +300,7 @@ def main_mel2wav(a):
             "config": {"workload": f"mel2wav B={B}/GPU, 80x{T} normalized mels, preprocess {PREPROCESS} "
                                    f"(assumed AdaIN-VC config)", "batch_per_gpu": B, "frames": T,
                        "parallelism": f"dp{world} (independent utterance shards, no collective)"},
-            "roofline": roof, "cpu_baseline": cpu}), flush=True)
+            "roofline": roof, "cpu_baseline": cpu, "front_end_wav2mel": front}), flush=True)
     if dist:
         dist.destroy_process_group()
 
