@@ -101,36 +101,26 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     const int ch0 = 32 * w + 4 * kq;                    // + 16*i + r
     constexpr int WPL = FZ_MASK_WORDS_PER_LAYER / 4;    // mask words per (layer, wave)
 
-    // ---- x -> XB (transposed, reflect rows).  16-byte loads, all of a thread's issued
-    // before any store (one HBM round trip, not one per element); 80*T is a multiple of 4
+    // ---- x -> XB (transposed, reflect rows).  Lane (t, half) of the 128 frame slots reads
+    // x[ci][t] for the VE channels of every other channel group (coalesced: two 128-B runs
+    // per wave load) and writes each group as ONE 16-byte LDS store.  A row is 2 mod 16
+    // 16-byte slots long, so the 16 lanes (8 frames x 2 halves) of a store phase hit 16
+    // distinct slots: conflict-free.  All loads are issued before any store (one HBM round
+    // trip); the first GEMM's weight ring is filled before them and lands meanwhile.
+    constexpr int NGX = FZ_CIN / VE;                    // 16-byte channel groups of a row
+    constexpr int GPT = NGX / 2;                        // groups per thread
+    static_assert(NGX % 2 == 0, "channel groups split over two lanes");
+    const int xt = 32 * w + (lane >> 1), xh = lane & 1;
+    float xv[GPT][VE];
     {
-        const f32x4* x4 = reinterpret_cast<const f32x4*>(A.x + (size_t)b * FZ_CIN * T);
-        const int n4 = FZ_CIN * T / 4;
-        constexpr int XV = (FZ_CIN * 128 / 4 + 255) / 256;   // f32x4 per thread at T <= 128
-        f32x4 xv[XV];
+        const float* xs = A.x + (size_t)b * FZ_CIN * T + xt;
+        if (xt < T) {
 #pragma unroll
-        for (int k = 0; k < XV; ++k) {
-            const int q = tid + 256 * k;
-            xv[k] = q < n4 ? x4[q] : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+            for (int m = 0; m < GPT; ++m)
 #pragma unroll
-        for (int k = 0; k < XV; ++k) {
-            const int q = tid + 256 * k;
-            if (q >= n4) continue;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int idx = 4 * q + e;
-                const int ci = idx / T, t = idx - ci * T;
-                const float v = xv[k][e];
-                st1<PREC>(XB + (4 + t) * RS + ci * ESZ, v);
-                if (t >= 1 && t <= 4) st1<PREC>(XB + (4 - t) * RS + ci * ESZ, v);
-                if (t >= T - 5 && t <= T - 2) st1<PREC>(XB + (4 + 2 * T - 2 - t) * RS + ci * ESZ, v);
-            }
+                for (int e = 0; e < VE; ++e) xv[m][e] = xs[(size_t)((2 * m + xh) * VE + e) * T];
         }
     }
-    __syncthreads();
-    FZ_PH();
-
     const auto nf0 = IC<G>{};
     const int ns_c = ks * FZ_C / KS;
     // the A operands of the pass, in launch order (each GEMM prefetches the next one's)
@@ -148,6 +138,26 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     auto op_mean = [&]() __attribute__((always_inline)) { return aop(A.w.mean_w, 2 * w, 2, FZ_C / KS, FZ_C / KS); };
     ARing<2> ring;
     ring_fill(ring, op_bank(0));
+    if (xt < T) {
+#pragma unroll
+        for (int m = 0; m < GPT; ++m) {
+            f32x4 v;
+            if constexpr (PREC == PREC_F32) {
+                v = f32x4{xv[m][0], xv[m][1], xv[m][2], xv[m][3]};
+            } else {
+                bf16x8 h;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) h[e] = (__bf16)xv[m][e];
+                v = __builtin_bit_cast(f32x4, h);
+            }
+            const int cb = (2 * m + xh) * 16;
+            *reinterpret_cast<f32x4*>(XB + (4 + xt) * RS + cb) = v;
+            if (xt >= 1 && xt <= 4) *reinterpret_cast<f32x4*>(XB + (4 - xt) * RS + cb) = v;
+            if (xt >= T - 5 && xt <= T - 2) *reinterpret_cast<f32x4*>(XB + (4 + 2 * T - 2 - xt) * RS + cb) = v;
+        }
+    }
+    __syncthreads();
+    FZ_PH();
     int rb[NF];
     f32x4 acc_h[2][NF];
     zero_acc(acc_h);
@@ -655,8 +665,12 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     FZ_PH();
 
     // deterministic cross-wave sum: ((p0 + p2) + (p1 + p3)), then tanh' + Adam
+    // rows padded by 4 floats at T = 128: the 4 lane groups (kq) of a store then start 16
+    // banks apart instead of on the same 16 banks (a 4-way conflict)
+    const int TP = STD ? T + 4 : T;
+    auto rq = [&](int q) __attribute__((always_inline)) { return STD ? q + q / (StdSE::T / 4) : q; };
     float* R0 = reinterpret_cast<float*>(fz_lds);
-    float* R1 = R0 + FZ_CIN * T;
+    float* R1 = R0 + FZ_CIN * TP;
     for (int phase = 0; phase < 2; ++phase) {
         // phase 0: waves 2, 3 store p2 -> R0, p3 -> R1;  phase 1: waves 0, 1 add p0, p1
         if ((phase == 0) == (w >= 2)) {
@@ -669,7 +683,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     if (t >= T) continue;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        float* p = R + (16 * i + 4 * kq + r) * T + t;
+                        float* p = R + (16 * i + 4 * kq + r) * TP + t;
                         *p = phase ? accx[i][f][r] + *p : accx[i][f][r];
                     }
                 }
@@ -682,7 +696,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         f32x4* gx = reinterpret_cast<f32x4*>(A.gx_out + (size_t)b * FZ_CIN * T);
         const f32x4* R04 = reinterpret_cast<const f32x4*>(R0);
         const f32x4* R14 = reinterpret_cast<const f32x4*>(R1);
-        for (int q = tid; q < FZ_CIN * T / 4; q += 256) gx[q] = R04[q] + R14[q];
+        for (int q = tid; q < FZ_CIN * T / 4; q += 256) gx[q] = R04[rq(q)] + R14[rq(q)];
         return;
     }
     const AdamArgs& Ad = A.adam;
@@ -690,6 +704,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const int step = min(max(*A.step, 1), A.table_len);
     const float nstep = Ad.table[2 * (step - 1)];
     const float bc2s = Ad.table[2 * (step - 1) + 1];
+    const float rbc2s = 1.f / bc2s;
     const size_t base4 = (size_t)b * FZ_CIN * T / 4;
     f32x4* __restrict__ ptb4 = reinterpret_cast<f32x4*>(Ad.ptb) + base4;
     f32x4* __restrict__ m4 = reinterpret_cast<f32x4*>(Ad.m) + base4;
@@ -717,17 +732,29 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         for (int k = 0; k < AB; ++k) {
             const int q = q0 + tid + 256 * k;
             if (q >= n4) continue;
-            const f32x4 gsum = R04[q] + R14[q];
+            const f32x4 gsum = R04[rq(q)] + R14[rq(q)];
             f32x4 p = P[k], mm = M[k], vv = V[k], g, ad;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float th = tanhf(p[e]);
+#if AVC_FZ_ABLATE & 8
+                // timing only: the tail without its transcendental / IEEE-division cost
+                const float th = p[e] * 0.5f;
                 g[e] = (gsum[e] * eps) * (1.f - th * th);
                 mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
                 vv[e] = vv[e] * Ad.b2;
                 vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
-                p[e] = p[e] + nstep * (mm[e] / (sqrtf(vv[e]) / bc2s + Ad.adam_eps));
-                ad[e] = X[k][e] + eps * tanhf(p[e]);
+                p[e] = p[e] + nstep * (mm[e] * (vv[e] * bc2s + Ad.adam_eps));
+                ad[e] = X[k][e] + eps * p[e] * 0.25f;
+#else
+                const float th = fast_tanh(p[e]);
+                g[e] = (gsum[e] * eps) * (1.f - th * th);
+                mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
+                vv[e] = vv[e] * Ad.b2;
+                vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
+                const float den = __builtin_amdgcn_sqrtf(vv[e]) * rbc2s + Ad.adam_eps;
+                p[e] = p[e] + nstep * (mm[e] * __builtin_amdgcn_rcpf(den));
+                ad[e] = X[k][e] + eps * fast_tanh(p[e]);
+#endif
             }
             if (g04) g04[q] = g;
             ptb4[q] = p;

@@ -426,6 +426,25 @@ struct MaskRd {
     }
 };
 
+// tanh for the Adam tail (attack_utils.py:77-78,86: eps * tanh(ptb)) on the hardware
+// exp2 / reciprocal instead of the libm sequence (the tail was VALU-bound on it: 2
+// tanh + sqrt + 2 IEEE divisions per element at one wave per SIMD).  |x| < 0.625: odd
+// polynomial x + x^3 P(x^2) (least-squares fit in relative error, <= 0.9 ulp in f32);
+// otherwise 1 - 2 / (1 + e^{2|x|}) (<= 2 ulp).  Parity: tests/test_gpu_*.py tolerances.
+__device__ __forceinline__ float fast_tanh(float x) {
+    const float a = __builtin_fabsf(x);
+    const float x2 = x * x;
+    float p = -0.005691935773938894f;
+    p = __builtin_fmaf(p, x2, 0.02062624879181385f);
+    p = __builtin_fmaf(p, x2, -0.05373530462384224f);
+    p = __builtin_fmaf(p, x2, 0.13331380486488342f);
+    p = __builtin_fmaf(p, x2, -0.3333328068256378f);
+    const float small = __builtin_fmaf(x * x2, p, x);
+    const float e = __builtin_amdgcn_exp2f(a * 2.8853900817779268f);   // 2 log2(e)
+    const float big = __builtin_copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e), x);
+    return a < 0.625f ? small : big;
+}
+
 // write 4 consecutive channels of frame t of a padded operand image (pad P rows each
 // side, reflect): row P+t, plus its mirror rows (F.pad reflect)
 template <int PREC>

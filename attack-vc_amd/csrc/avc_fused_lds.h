@@ -14,7 +14,7 @@ __host__ __device__ constexpr int fz_lds_fwd(int prec, int T, int ks) {
 // blocks: two dY images; bank: g_pre0 image + bank dY image; reduction: two [80][T] fp32
 __host__ __device__ constexpr int fz_lds_bwd_main(int prec, int T) {
     return fz_max2(fz_max2(2 * (T + 8) * fz_rs(prec), (T + 8) * fz_rs(prec) + (T + 16) * fz_rs(prec)),
-                   2 * FZ_CIN * T * 4);
+                   2 * FZ_CIN * (T + 4) * 4);   // rows padded at T = 128 (avc_fused.hip)
 }
 // + per-wave fold scratch [5*16 ch][8 edge columns] fp32
 __host__ __device__ constexpr int fz_lds_bwd(int prec, int T) { return fz_lds_bwd_main(prec, T) + 4 * 5 * 16 * 8 * 4; }
