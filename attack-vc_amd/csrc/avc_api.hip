@@ -130,6 +130,7 @@ struct Workspace {
     std::vector<DevBuf> a1, a2, hb;   // per block
     DevBuf losses, table, scal, slab;
     DevBuf pooled, gpooled;           // fused path: [B][128] time-mean of h_N and its gradient
+    DevBuf loss_cur;                  // fused head: [B] per-utterance loss of the current iteration
     unsigned long long* masks = nullptr;   // fused path: ReLU' ballot words [B][mask_words]
     int mask_words = 0;
     bool fused = false;               // this (B, T) runs on the fused engine
@@ -660,7 +661,7 @@ static void free_plans(Workspace& ws) {
 static void free_ws(Workspace& ws) {
     free_plans(ws);
     DevBuf* bufs[] = {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.bank, &ws.h0, &ws.gbank, &ws.gxd,
-                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal, &ws.slab, &ws.pooled, &ws.gpooled};
+                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal, &ws.slab, &ws.pooled, &ws.gpooled, &ws.loss_cur};
     for (DevBuf* b : bufs) dfree(*b);
     for (auto& b : ws.a1) dfree(b);
     for (auto& b : ws.a2) dfree(b);
@@ -1087,60 +1088,74 @@ static int fused_shape(avc_ctx* ctx, int T) {
 static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, bool attack, int prec) {
     const avc_se_cfg& c = ctx->cfg;
     const int B = ws.B;
-    {
-        Launch L;
-        L.kind = L_FZ_FWD;
-        L.prec = prec;
-        L.grid = dim3(B);
-        L.block = dim3(256);
-        L.shmem = fz_lds_fwd(prec, ws.T, c.kernel_size);
-        L.fz = fused_args(ctx, ws, prec);
-        L.fz.x = x;
-        L.fz.write_masks = attack ? 1 : 0;
-        L.fz.tick = attack ? ws.step : nullptr;
-        L.fz_shape = fused_shape(ctx, ws.T);
-        L.flop = fz_fwd_flop(c, ws.Tl, ctx->bank_k) * B;
-        L.name = prec == PREC_F32 ? "se_fwd_fused<f32>" : "se_fwd_fused<bf16>";
-        pl.launches.push_back(L);
+    Launch F;
+    F.kind = L_FZ_FWD;
+    F.prec = prec;
+    F.grid = dim3(B);
+    F.block = dim3(256);
+    F.shmem = fz_lds_fwd(prec, ws.T, c.kernel_size);
+    F.fz = fused_args(ctx, ws, prec);
+    F.fz.x = x;
+    F.fz.write_masks = attack ? 1 : 0;
+    F.fz.tick = attack ? ws.step : nullptr;
+    F.fz_shape = fused_shape(ctx, ws.T);
+    F.flop = fz_fwd_flop(c, ws.Tl, ctx->bank_k) * B;
+    F.name = prec == PREC_F32 ? "se_fwd_fused<f32>" : "se_fwd_fused<bf16>";
+
+    Launch L;
+    L.kind = L_HEAD_V;
+    L.grid = dim3(cdiv(B, 2));
+    L.block = dim3(512);
+    const int S = std::max(c.c_h, c.c_out);
+    L.shmem = (size_t)(2 * c.n_dense_blocks + 5) * S * 2 * sizeof(float) +
+              (size_t)(2 * c.n_dense_blocks * c.c_h + c.c_out + 4 * c.c_out + 2) * sizeof(float);
+    HeadArgs& A = L.head;
+    L.prec = prec;
+    A.Wr = ctx->head_Wr.p;
+    A.WrT = ctx->head_WrT.p;
+    A.Wr16 = reinterpret_cast<const uint16_t*>(ctx->head_Wr16.p);
+    A.WrT16 = reinterpret_cast<const uint16_t*>(ctx->head_WrT16.p);
+    A.pooled_in = ws.pooled.p;
+    A.g_pooled = attack ? ws.gpooled.p : nullptr;
+    A.Wp = ctx->head_Wp.p;
+    A.WpT = ctx->head_WpT.p;
+    A.bias = ctx->head_bias.p;
+    A.emb_out = ws.emb_fwd.p;
+    A.tgt = ws.tgt.p;
+    A.org = ws.org.p;
+    A.losses = ws.losses.p;
+    A.step = ws.step;
+    A.B = B;
+    A.C = c.c_h;
+    A.TN = ws.Tl[c.n_conv_blocks];
+    A.D = c.c_out;
+    A.n_dense = c.n_dense_blocks;
+    A.act = c.act;
+    A.mode = attack ? 1 : 0;
+    A.scal = ws.scal.p;
+    A.loss_len = ws.iters_cap;
+    const double dense = 2.0 * c.c_h * c.c_h * 2 * c.n_dense_blocks + 2.0 * c.c_out * c.c_h;
+    L.flop = dense * B * (attack ? 2 : 1);
+    L.name = "se_head_v";
+
+    // emb attack in bf16: the head runs in the forward's tail (se_head_fused), one launch
+    // fewer per iteration; AVC_FUSE_HEAD=0 keeps the separate se_head_v launch (A/B runs)
+    const char* fe = getenv("AVC_FUSE_HEAD");
+    // (standard shape only: the in-kernel chain is unrolled for its n_dense = 6)
+    if (attack && prec == PREC_BF16 && ctx->head_Wr16.p && c.c_h == FZ_C && c.c_out == FZ_C && F.fz_shape == 0 &&
+        c.n_dense_blocks == 6 && !(fe && fe[0] == '0')) {
+        const size_t head_lds = (size_t)(4 * c.n_dense_blocks + 8) * FZ_C * sizeof(float);
+        F.shmem = std::max(F.shmem, head_lds);
+        F.fz.fuse_head = 1;
+        F.fz.head = A;
+        F.fz.loss_cur = ws.loss_cur.p;
+        F.flop += L.flop;
+        F.name = "se_fwd_fused<bf16>";
+        pl.launches.push_back(F);
+        return 0;
     }
-    {
-        Launch L;
-        L.kind = L_HEAD_V;
-        L.grid = dim3(cdiv(B, 2));
-        L.block = dim3(512);
-        const int S = std::max(c.c_h, c.c_out);
-        L.shmem = (size_t)(2 * c.n_dense_blocks + 5) * S * 2 * sizeof(float) +
-                  (size_t)(2 * c.n_dense_blocks * c.c_h + c.c_out + 4 * c.c_out + 2) * sizeof(float);
-        HeadArgs& A = L.head;
-        L.prec = prec;
-        A.Wr = ctx->head_Wr.p;
-        A.WrT = ctx->head_WrT.p;
-        A.Wr16 = reinterpret_cast<const uint16_t*>(ctx->head_Wr16.p);
-        A.WrT16 = reinterpret_cast<const uint16_t*>(ctx->head_WrT16.p);
-        A.pooled_in = ws.pooled.p;
-        A.g_pooled = attack ? ws.gpooled.p : nullptr;
-        A.Wp = ctx->head_Wp.p;
-        A.WpT = ctx->head_WpT.p;
-        A.bias = ctx->head_bias.p;
-        A.emb_out = ws.emb_fwd.p;
-        A.tgt = ws.tgt.p;
-        A.org = ws.org.p;
-        A.losses = ws.losses.p;
-        A.step = ws.step;
-        A.B = B;
-        A.C = c.c_h;
-        A.TN = ws.Tl[c.n_conv_blocks];
-        A.D = c.c_out;
-        A.n_dense = c.n_dense_blocks;
-        A.act = c.act;
-        A.mode = attack ? 1 : 0;
-        A.scal = ws.scal.p;
-        A.loss_len = ws.iters_cap;
-        const double dense = 2.0 * c.c_h * c.c_h * 2 * c.n_dense_blocks + 2.0 * c.c_out * c.c_h;
-        L.flop = dense * B * (attack ? 2 : 1);
-        L.name = "se_head_v";
-        pl.launches.push_back(L);
-    }
+    pl.launches.push_back(F);
+    pl.launches.push_back(L);
     return 0;
 }
 
@@ -1173,7 +1188,19 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
 
 static int plan_iteration(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) {
     if (ws.fused)
-        return plan_fused_forward(ctx, ws, pl, ws.adv.p, true, prec) || plan_fused_backward(ctx, ws, pl, prec);
+    {
+        if (plan_fused_forward(ctx, ws, pl, ws.adv.p, true, prec) || plan_fused_backward(ctx, ws, pl, prec)) return 1;
+        // a forward with the head fused hands its per-utterance loss to the backward, which
+        // knows the step (the forward's block 0 advances the counter while it runs)
+        const Launch& F = pl.launches[pl.launches.size() - 2];
+        if (F.kind == L_FZ_FWD && F.fz.fuse_head) {
+            Launch& Bk = pl.launches.back();
+            Bk.fz.loss_cur = ws.loss_cur.p;
+            Bk.fz.losses = ws.losses.p;
+            Bk.fz.loss_len = ws.iters_cap;
+        }
+        return 0;
+    }
     return plan_forward(ctx, ws, pl, ws.adv.p, true, prec) || plan_backward(ctx, ws, pl, prec);
 }
 
@@ -1231,6 +1258,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
             ws.mask_words = (nb + 1 + 2 * c.n_conv_blocks) * FZ_MASK_WORDS_PER_LAYER;
             rc |= dalloc(ws.pooled, (size_t)B * FZ_C);
             rc |= dalloc(ws.gpooled, (size_t)B * FZ_C);
+            rc |= dalloc(ws.loss_cur, (size_t)B);
             HIPCHK(hipMalloc(&ws.masks, (size_t)B * ws.mask_words * sizeof(unsigned long long)));
         } else {
             rc |= dalloc(ws.gxd, X);

@@ -51,7 +51,7 @@ namespace avc {
 // guards produced wrong results on gfx950 for one-fragment layers.
 // ---------------------------------------------------------------------------------
 struct StdSE {
-    static constexpr int T = 128, NB = 8, KSZ = 5, NBLK = 6;
+    static constexpr int T = 128, NB = 8, KSZ = 5, NBLK = 6, NDENSE = 6;
     static constexpr int sub(int l) { return (l & 1) ? 2 : 1; }
     static constexpr int Tl(int l) {
         int t = T;
@@ -61,6 +61,180 @@ struct StdSE {
     static constexpr int nf(int frames) { return (frames + 15) / 16; }
 };
 
+
+// ---------------------------------------------------------------------------------
+// Embedding-attack head in the forward's tail (bf16 mode, c_h = c_out = 128): time-mean
+// -> 2*nd dense layers -> output Linear -> loss (attack_utils.py:81-82) -> backward to
+// d loss / d time-mean, for THIS workgroup's utterance.  The same chain, per-element
+// arithmetic and summation order as se_head_v mode 1 (avc_kernels.hip), which it
+// replaces for the emb attack: that launch is a latency-bound 26-step chain on 128 CUs
+// between the two conv kernels; here every CU streams the 13 matrices itself (832 KB of
+// bf16 per utterance) while its conv-stack LDS is dead.  Thread u owns rows u/4 and
+// u/4 + 64 with K slice u%4 -- se_head_v's threads u and u + 256 -- so se_head_v's
+// packed bf16 weights are used as they are.
+// ---------------------------------------------------------------------------------
+typedef unsigned hu32x4 __attribute__((ext_vector_type(4)));
+struct HW16 {
+    hu32x4 r[4];   // 32 bf16 weights of one row slice, 8 per 16-byte chunk
+};
+__device__ __forceinline__ float hw16_w(const HW16& hw, int e, int j) {
+    const int f = 4 * e + j, cc = f >> 3, i = f & 7;
+    const unsigned word = hw.r[cc][i >> 1];
+    return __builtin_bit_cast(float, (i & 1) ? (word & 0xffff0000u) : (word << 16));
+}
+// sum_k W[m][k] X[k] over this lane's K slice, then over the row's 4 slices (DPP)
+__device__ __forceinline__ float head_dot(const HW16& hw, const float* X, int q) {
+#pragma clang fp contract(off)
+    float acc = 0.f, acc2 = 0.f;   // even / odd k of each pair (se_head_v's order)
+    const f32x2* X2 = reinterpret_cast<const f32x2*>(X);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x2 x = X2[4 * (2 * e + h) + q];   // k = 8i + 2q, i = 2e + h
+            acc = fmaf(hw16_w(hw, e, 2 * h), x[0], acc);
+            acc2 = fmaf(hw16_w(hw, e, 2 * h + 1), x[1], acc2);
+        }
+    acc = acc + acc2;
+    acc += dpp_mov<0xB1>(acc);
+    acc += dpp_mov<0x4E>(acc);
+    return acc;
+}
+// sm: LDS floats, E (the time-mean, [128]) already written by the caller.  ND = n_dense
+// (compile-time: the 2*(2*ND+1) chain steps are straight-line code, so the 3-step weight
+// ring stays in flight across the per-step barriers -- a runtime loop made the compiler
+// copy the ring registers at the loop head and drain it with vmcnt(0) every iteration).
+// Per-row state a thread needs again (biases, targets, the forward activations for the
+// act' masks, E and GB of its own rows) stays in registers; LDS only carries the vectors
+// every thread reads (E, Y_i, GA, GM).
+template <int ND>
+__device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* sm, float* loss_cur) {
+#pragma clang fp contract(off)
+    constexpr int C = FZ_C, D = FZ_C;
+    constexpr size_t CC = (size_t)C * C;
+    constexpr int NF = 2 * ND + 1, NL = 2 * NF;
+    const int act = H.act;
+    const int tid = threadIdx.x, q = tid & 3, m0 = tid >> 2, ln = tid & 63, wv = tid >> 6;
+    const bool own = q == 0;
+    float* E = sm;
+    float* Ys = E + C;                 // [2ND][C]
+    float* GA = Ys + 2 * ND * C;
+    float* GB = GA + C;                // loss scratch only
+    float* GM = GB + C;
+    float* LS = GM + C;
+    const uint16_t* __restrict__ W16 = H.Wr16;
+    const uint16_t* __restrict__ WT16 = H.WrT16;
+    // rows m0 (se_head_v thread tid: wave wv) and m0 + 64 (thread tid + 256: wave wv + 4)
+    auto load_w = [&](HW16 (&hw)[2], auto I) __attribute__((always_inline)) {
+        constexpr int i = decltype(I)::value;
+        constexpr int j = i - NF - 1, l = ND - 1 - j / 2;
+        const uint16_t* base = i < NF ? W16 + (size_t)i * CC                       // dense, then output
+                                      : (i == NF ? WT16 + (size_t)(2 * ND) * CC     // output^T
+                                                 : WT16 + (size_t)(j % 2 == 0 ? 2 * l + 1 : 2 * l) * CC);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+#if AVC_FZ_ABLATE & 16
+                hw[h].r[cc] = hu32x4{(unsigned)i, 3u, 5u, (unsigned)cc};   // timing only: no weight loads
+#else
+                hw[h].r[cc] = gload<hu32x4>(reinterpret_cast<const float*>(
+                    base + ((size_t)((wv + 4 * h) * 4 + cc) * 64 + ln) * 8));
+#endif
+    };
+    float bias[NF][2], tg[2], og[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int m = m0 + 64 * h;
+#pragma unroll
+        for (int i = 0; i < NF; ++i) bias[i][h] = H.bias[i * C + m];
+        tg[h] = H.tgt[(size_t)b * D + m];
+        og[h] = H.org[(size_t)b * D + m];
+    }
+    const float gscale = H.scal[1];
+    HW16 w0[2], w1[2], w2[2];
+    load_w(w0, IC<0>{});
+    load_w(w1, IC<1>{});
+    load_w(w2, IC<2>{});
+    __syncthreads();
+    float e_own[2], gb_own[2] = {0.f, 0.f}, ys[2 * ND][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) e_own[h] = E[m0 + 64 * h];
+
+    auto run_step = [&](auto I, const HW16 (&hw)[2]) __attribute__((always_inline)) {
+        constexpr int i = decltype(I)::value;
+        constexpr int j = i - NF - 1, l = ND - 1 - j / 2;
+        const float* X = i < 2 * ND ? ((i % 2 == 0) ? E : Ys + (i - 1) * C)
+                                    : (i == 2 * ND ? E : (i == NF ? GA : (j % 2 == 0 ? GM : GA)));
+        float o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) o[h] = head_dot(hw[h], X, q);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int m = m0 + 64 * h;
+            if constexpr (i < 2 * ND) {
+                const float y = act_f(o[h] + bias[i][h], act);
+                ys[i][h] = y;
+                if (own) Ys[i * C + m] = y;
+                if constexpr (i % 2 == 1) {
+                    e_own[h] = y + e_own[h];
+                    if (own) E[m] = e_own[h];
+                }
+            } else if constexpr (i == 2 * ND) {
+                // loss = MSE(emb, tgt) - 0.1 MSE(emb, org) (attack_utils.py:81-82)
+                const float e = o[h] + bias[2 * ND][h];
+                const float d1 = e - tg[h], d2 = e - og[h];
+                if (own) {
+                    GA[m] = gscale * d1 + gscale * d2 * -0.1f;
+                    GB[m] = d1 * d1;
+                    GM[m] = d2 * d2;
+                }
+            } else if constexpr (i == NF) {
+                gb_own[h] = o[h];
+                if (own) GM[m] = o[h] * act_d(ys[2 * ND - 1][h], act);
+            } else if constexpr (j % 2 == 0) {
+                if (own) GA[m] = o[h] * act_d(ys[2 * l][h], act);
+            } else {
+                gb_own[h] = gb_own[h] + o[h];
+                if constexpr (l > 0)
+                    if (own) GM[m] = gb_own[h] * act_d(ys[2 * l - 1][h], act);
+            }
+        }
+        if constexpr (i == 2 * ND) {
+            __syncthreads();
+            if (tid < 64) {   // per-utterance loss, fixed summation order (se_head_v's)
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int d = 0; d < D; d += 64) {
+                    s1 += GB[d + tid];
+                    s2 += GM[d + tid];
+                }
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    s1 += __shfl_xor(s1, off);
+                    s2 += __shfl_xor(s2, off);
+                }
+                if (tid == 0) LS[0] = s1 / (float)D - 0.1f * (s2 / (float)D);
+            }
+        }
+        __syncthreads();
+    };
+    // 3-step register ring: slot i % 3 holds step i and is refilled with step i + 3
+    static_for<0, NL>([&](auto I) __attribute__((always_inline)) {
+        constexpr int i = decltype(I)::value;
+        auto step = [&](HW16 (&slot)[2]) __attribute__((always_inline)) {
+            run_step(I, slot);
+            if constexpr (i + 3 < NL) load_w(slot, IC<i + 3>{});
+        };
+        if constexpr (i % 3 == 0) step(w0);
+        else if constexpr (i % 3 == 1) step(w1);
+        else step(w2);
+    });
+    if (own)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) H.g_pooled[(size_t)b * C + m0 + 64 * h] = gb_own[h];
+    if (tid == 0) loss_cur[b] = LS[0];
+}
 
 // ---------------------------------------------------------------------------------
 // forward
@@ -390,6 +564,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         return;
     }
     // AdaptiveAvgPool1d(1): mean over the TN frames of each channel
+    float* hsm = reinterpret_cast<float*>(fz_lds);      // fused head's LDS (conv images dead)
+    const bool fh = PREC == PREC_BF16 && A.fuse_head != 0;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
@@ -402,9 +578,16 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) m[r] = s4[r] / (float)TN;
             *reinterpret_cast<f32x4*>(A.pooled + (size_t)b * FZ_C + ch0 + 16 * i) = m;
+            if (fh) *reinterpret_cast<f32x4*>(hsm + ch0 + 16 * i) = m;
         }
     }
     FZ_PH();
+    if constexpr (PREC == PREC_BF16) {
+        if (fh) {
+            if constexpr (STD != 0) se_head_fused<StdSE::NDENSE>(A.head, b, hsm, A.loss_cur);
+            FZ_PH();
+        }
+    }
     FZ_PH_DUMP("fwd");
 }
 
@@ -701,6 +884,10 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     }
     const AdamArgs& Ad = A.adam;
     const float eps = A.scal[0];
+    if (A.losses && tid == 0) {   // the fused head's loss of this iteration -> history row step-1
+        const int sn = *A.step;
+        if (sn >= 1 && sn <= A.loss_len) A.losses[(size_t)(sn - 1) * A.B + b] = A.loss_cur[b];
+    }
     const int step = min(max(*A.step, 1), A.table_len);
     const float nstep = Ad.table[2 * (step - 1)];
     const float bc2s = Ad.table[2 * (step - 1) + 1];

@@ -164,6 +164,12 @@ struct FusedArgs {
     float* gx_out;                    // bwd: if set, write d loss / d x [B][80][T] here (no Adam)
     AdamArgs adam;                    // bwd: Adam update + next adv
     FusedW w;
+    // emb attack, bf16: the head chain (se_head_v mode 1) runs in the forward's tail
+    int32_t fuse_head;                // fwd: run `head` for this workgroup's utterance
+    int32_t loss_len;                 // bwd: rows of `losses`
+    float* loss_cur;                  // fwd writes / bwd reads: [B] this iteration's per-utterance loss
+    float* losses;                    // bwd: [loss_len][B] loss history (row = step - 1), or null
+    HeadArgs head;                    // fwd (fuse_head): weights, biases, targets, g_pooled out
 };
 
 // ---------------------------------------------------------------------------------
