@@ -275,6 +275,23 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     const int ch0 = 32 * w + 4 * kq;                    // + 16*i + r
     constexpr int WPL = FZ_MASK_WORDS_PER_LAYER / 4;    // mask words per (layer, wave)
 
+    const auto nf0 = IC<G>{};
+    const int ns_c = ks * FZ_C / KS;
+    // the A operands of the pass, in launch order (each GEMM prefetches the next one's)
+    auto op_bank = [&](int kb) __attribute__((always_inline)) {
+        const int ns = (FZ_CIN * (kb + 1) + KS - 1) / KS;
+        return aop(A.w.bank[kb], 2 * w, 2, ns, ns);
+    };
+    auto op_inb = [&](int kb) __attribute__((always_inline)) { return aop(A.w.in_b[kb], 2 * w, 2, FZ_C / KS, FZ_C / KS); };
+    auto op_inx = [&]() __attribute__((always_inline)) {
+        const int ns = (FZ_CIN + KS - 1) / KS;
+        return aop(A.w.in_x, 2 * w, 2, ns, ns);
+    };
+    auto op_c1 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_mean = [&]() __attribute__((always_inline)) { return aop(A.w.mean_w, 2 * w, 2, FZ_C / KS, FZ_C / KS); };
+    ARing<2> ring;
+    ring_fill(ring, op_bank(0));
     // ---- x -> XB (transposed, reflect rows).  Lane (t, half) of the 128 frame slots reads
     // x[ci][t] for the VE channels of every other channel group (coalesced: two 128-B runs
     // per wave load) and writes each group as ONE 16-byte LDS store.  A row is 2 mod 16
@@ -295,23 +312,6 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
                 for (int e = 0; e < VE; ++e) xv[m][e] = xs[(size_t)((2 * m + xh) * VE + e) * T];
         }
     }
-    const auto nf0 = IC<G>{};
-    const int ns_c = ks * FZ_C / KS;
-    // the A operands of the pass, in launch order (each GEMM prefetches the next one's)
-    auto op_bank = [&](int kb) __attribute__((always_inline)) {
-        const int ns = (FZ_CIN * (kb + 1) + KS - 1) / KS;
-        return aop(A.w.bank[kb], 2 * w, 2, ns, ns);
-    };
-    auto op_inb = [&](int kb) __attribute__((always_inline)) { return aop(A.w.in_b[kb], 2 * w, 2, FZ_C / KS, FZ_C / KS); };
-    auto op_inx = [&]() __attribute__((always_inline)) {
-        const int ns = (FZ_CIN + KS - 1) / KS;
-        return aop(A.w.in_x, 2 * w, 2, ns, ns);
-    };
-    auto op_c1 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1[l], 2 * w, 2, ns_c, ns_c); };
-    auto op_c2 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2[l], 2 * w, 2, ns_c, ns_c); };
-    auto op_mean = [&]() __attribute__((always_inline)) { return aop(A.w.mean_w, 2 * w, 2, FZ_C / KS, FZ_C / KS); };
-    ARing<2> ring;
-    ring_fill(ring, op_bank(0));
     if (xt < T) {
 #pragma unroll
         for (int m = 0; m < GPT; ++m) {
@@ -622,6 +622,22 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const u64* mbase = A.masks + (size_t)b * A.mask_words;
     auto mwords = [&](int layer) __attribute__((always_inline)) { return mbase + (size_t)(layer * 4 + w) * WPL; };
 
+    // g_pooled, then the first GEMM's weight ring and mask words, are issued before the
+    // LDS clearing so their latency hides under it
+    const int TN = STD ? StdSE::Tl(StdSE::NBLK) : A.Tl[A.nblk];
+    f32x4 gp[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) gp[i] = *reinterpret_cast<const f32x4*>(A.g_pooled + (size_t)b * FZ_C + ch0 + 16 * i);
+    const int ns_c = ks * FZ_C / KS;
+    const int nblk = STD ? StdSE::NBLK : A.nblk;
+    auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2T[l], 2 * w, 2, ns_c, ns_c); };
+    ARing<2> ring;
+    ring_fill(ring, op_c2T(nblk - 1));
+    // ReLU' words of the next layer whose mask is applied, loaded one GEMM ahead
+    MaskRd mnext;
+    mnext.load(mwords(nb + 2 + 2 * (nblk - 1)));
+
     char* GB = fz_lds;                          // dilated dY image [T+2ZP] rows
     char* GB2 = GB + (T + 2 * ZP) * RS;         // stride-1 dY image [T+2ZP] rows
     float* FSCR = reinterpret_cast<float*>(fz_lds + fz_lds_bwd_main(PREC, T)) + w * (5 * 16 * 8);
@@ -631,11 +647,10 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     }
 
     // g(h_N): d mean / d h = 1/TN on the TN valid frames
-    const int TN = STD ? StdSE::Tl(StdSE::NBLK) : A.Tl[A.nblk];
     f32x4 gh[2][NF];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        f32x4 g = *reinterpret_cast<const f32x4*>(A.g_pooled + (size_t)b * FZ_C + ch0 + 16 * i);
+        f32x4 g = gp[i];
 #pragma unroll
         for (int r = 0; r < 4; ++r) g[r] = g[r] / (float)TN;
 #pragma unroll
@@ -644,16 +659,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     __syncthreads();
     FZ_PH();
 
-    const int ns_c = ks * FZ_C / KS;
-    const int nblk = STD ? StdSE::NBLK : A.nblk;
-    auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
-    auto op_c2T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2T[l], 2 * w, 2, ns_c, ns_c); };
-    ARing<2> ring;
-    ring_fill(ring, op_c2T(nblk - 1));
     int rb[NF];
-    // ReLU' words of the next layer whose mask is applied, loaded one GEMM ahead
-    MaskRd mnext;
-    mnext.load(mwords(nb + 2 + 2 * (nblk - 1)));
     // backward of one conv block; nfo: fragments of its output frames, nfc: of the
     // dgrad columns (Ti interior frames + 2P pad positions)
     auto block = [&](auto nfo, auto nfc, int l, int Ti, int To, int s) __attribute__((always_inline)) {
