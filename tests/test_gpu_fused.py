@@ -147,3 +147,26 @@ def test_bf16_objective_after_1500(full):
     l0 = ((ctx.se_forward(vc) - tgt) ** 2).mean(1)
     assert (l32 < l0).all() and (l16 < l0).all()          # both attacks made progress
     assert float(((l16 - l32).abs() / l32).max()) <= 0.05, (l16, l32)
+
+
+def test_fused_head_matches_separate_head(full, monkeypatch):
+    """The bf16 emb attack runs the head chain (dense blocks, output Linear, loss and its
+    backward) inside se_fwd_fused (se_head_fused); AVC_FUSE_HEAD=0 plans the separate
+    se_head_v launch instead.  Same per-element arithmetic in the same order, so adv, the
+    per-iteration losses (handed to the backward through a [B] buffer) and grad0 are
+    bitwise equal."""
+    z, m, ctx = full
+    g = torch.Generator().manual_seed(41)
+    vc, at, p0 = (torch.randn(6, 80, 128, generator=g).to(DEV) for _ in range(3))
+    ctx.set_engine("fused")
+    a, L, g0 = ctx.emb_attack(vc, at, p0, 0.1, 12, precision="bf16", want_losses=True, want_grad0=True)
+    ctx.set_engine("auto")
+    monkeypatch.setenv("AVC_FUSE_HEAD", "0")
+    sep = avc_native.Context(avc_native.se_config(m.speaker_encoder), avc_native.flat_weights(m.speaker_encoder),
+                             DEV.index or 0)
+    sep.set_engine("fused")
+    a2, L2, g02 = sep.emb_attack(vc, at, p0, 0.1, 12, precision="bf16", want_losses=True, want_grad0=True)
+    assert torch.isfinite(L).all() and L.abs().sum() > 0
+    assert torch.equal(a, a2)
+    assert torch.equal(L, L2)
+    assert torch.equal(g0, g02)
