@@ -82,19 +82,26 @@ __device__ __forceinline__ float hw16_w(const HW16& hw, int e, int j) {
     const unsigned word = hw.r[cc][i >> 1];
     return __builtin_bit_cast(float, (i & 1) ? (word & 0xffff0000u) : (word << 16));
 }
+// Head vectors in LDS are stored slice-major: element k at hpos(k) = q*36 + 2i + e
+// (k = 8i + 2q + e), so slice q's 32 inputs are one contiguous run read as eight
+// 16-byte loads; the 36-float slice stride puts the four slices of a wave's broadcast
+// reads on distinct banks.
+constexpr int HVS = 4 * 36;   // floats per head vector
+__device__ __forceinline__ int hpos(int k) { return ((k >> 1) & 3) * 36 + 2 * (k >> 3) + (k & 1); }
 // sum_k W[m][k] X[k] over this lane's K slice, then over the row's 4 slices (DPP)
 __device__ __forceinline__ float head_dot(const HW16& hw, const float* X, int q) {
 #pragma clang fp contract(off)
     float acc = 0.f, acc2 = 0.f;   // even / odd k of each pair (se_head_v's order)
-    const f32x2* X2 = reinterpret_cast<const f32x2*>(X);
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X + q * 36);
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
+    for (int e = 0; e < 8; ++e) {
+        const f32x4 x = X4[e];     // pairs i = 2e (x0, x1) and i = 2e + 1 (x2, x3), k = 8i + 2q
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const f32x2 x = X2[4 * (2 * e + h) + q];   // k = 8i + 2q, i = 2e + h
-            acc = fmaf(hw16_w(hw, e, 2 * h), x[0], acc);
-            acc2 = fmaf(hw16_w(hw, e, 2 * h + 1), x[1], acc2);
+            acc = fmaf(hw16_w(hw, e, 2 * h), x[2 * h], acc);
+            acc2 = fmaf(hw16_w(hw, e, 2 * h + 1), x[2 * h + 1], acc2);
         }
+    }
     acc = acc + acc2;
     acc += dpp_mov<0xB1>(acc);
     acc += dpp_mov<0x4E>(acc);
@@ -116,12 +123,12 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
     const int act = H.act;
     const int tid = threadIdx.x, q = tid & 3, m0 = tid >> 2, ln = tid & 63, wv = tid >> 6;
     const bool own = q == 0;
-    float* E = sm;
-    float* Ys = E + C;                 // [2ND][C]
-    float* GA = Ys + 2 * ND * C;
-    float* GB = GA + C;                // loss scratch only
-    float* GM = GB + C;
-    float* LS = GM + C;
+    float* E = sm;                     // head vectors: HVS floats each, slice-major (hpos)
+    float* Ys = E + HVS;               // [2ND][HVS]
+    float* GA = Ys + 2 * ND * HVS;
+    float* GB = GA + HVS;              // loss scratch only
+    float* GM = GB + HVS;
+    float* LS = GM + HVS;
     const uint16_t* __restrict__ W16 = H.Wr16;
     const uint16_t* __restrict__ WT16 = H.WrT16;
     // rows m0 (se_head_v thread tid: wave wv) and m0 + 64 (thread tid + 256: wave wv + 4)
@@ -159,12 +166,12 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
     __syncthreads();
     float e_own[2], gb_own[2] = {0.f, 0.f}, ys[2 * ND][2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) e_own[h] = E[m0 + 64 * h];
+    for (int h = 0; h < 2; ++h) e_own[h] = E[hpos(m0 + 64 * h)];
 
     auto run_step = [&](auto I, const HW16 (&hw)[2]) __attribute__((always_inline)) {
         constexpr int i = decltype(I)::value;
         constexpr int j = i - NF - 1, l = ND - 1 - j / 2;
-        const float* X = i < 2 * ND ? ((i % 2 == 0) ? E : Ys + (i - 1) * C)
+        const float* X = i < 2 * ND ? ((i % 2 == 0) ? E : Ys + (i - 1) * HVS)
                                     : (i == 2 * ND ? E : (i == NF ? GA : (j % 2 == 0 ? GM : GA)));
         float o[2];
 #pragma unroll
@@ -175,29 +182,29 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
             if constexpr (i < 2 * ND) {
                 const float y = act_f(o[h] + bias[i][h], act);
                 ys[i][h] = y;
-                if (own) Ys[i * C + m] = y;
+                if (own) Ys[i * HVS + hpos(m)] = y;
                 if constexpr (i % 2 == 1) {
                     e_own[h] = y + e_own[h];
-                    if (own) E[m] = e_own[h];
+                    if (own) E[hpos(m)] = e_own[h];
                 }
             } else if constexpr (i == 2 * ND) {
                 // loss = MSE(emb, tgt) - 0.1 MSE(emb, org) (attack_utils.py:81-82)
                 const float e = o[h] + bias[2 * ND][h];
                 const float d1 = e - tg[h], d2 = e - og[h];
                 if (own) {
-                    GA[m] = gscale * d1 + gscale * d2 * -0.1f;
-                    GB[m] = d1 * d1;
-                    GM[m] = d2 * d2;
+                    GA[hpos(m)] = gscale * d1 + gscale * d2 * -0.1f;
+                    GB[hpos(m)] = d1 * d1;
+                    GM[hpos(m)] = d2 * d2;
                 }
             } else if constexpr (i == NF) {
                 gb_own[h] = o[h];
-                if (own) GM[m] = o[h] * act_d(ys[2 * ND - 1][h], act);
+                if (own) GM[hpos(m)] = o[h] * act_d(ys[2 * ND - 1][h], act);
             } else if constexpr (j % 2 == 0) {
-                if (own) GA[m] = o[h] * act_d(ys[2 * l][h], act);
+                if (own) GA[hpos(m)] = o[h] * act_d(ys[2 * l][h], act);
             } else {
                 gb_own[h] = gb_own[h] + o[h];
                 if constexpr (l > 0)
-                    if (own) GM[m] = gb_own[h] * act_d(ys[2 * l - 1][h], act);
+                    if (own) GM[hpos(m)] = gb_own[h] * act_d(ys[2 * l - 1][h], act);
             }
         }
         if constexpr (i == 2 * ND) {
@@ -206,8 +213,8 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
                 float s1 = 0.f, s2 = 0.f;
 #pragma unroll
                 for (int d = 0; d < D; d += 64) {
-                    s1 += GB[d + tid];
-                    s2 += GM[d + tid];
+                    s1 += GB[hpos(d + tid)];
+                    s2 += GM[hpos(d + tid)];
                 }
 #pragma unroll
                 for (int off = 32; off >= 1; off >>= 1) {
@@ -578,7 +585,9 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) m[r] = s4[r] / (float)TN;
             *reinterpret_cast<f32x4*>(A.pooled + (size_t)b * FZ_C + ch0 + 16 * i) = m;
-            if (fh) *reinterpret_cast<f32x4*>(hsm + ch0 + 16 * i) = m;
+            if (fh)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) hsm[hpos(ch0 + 16 * i + rr)] = m[rr];
         }
     }
     FZ_PH();
