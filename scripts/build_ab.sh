@@ -10,7 +10,7 @@ for f in $(git ls-tree --name-only $REV attack-vc_amd/csrc/); do git show $REV:$
 git show $REV:include/avc.h > $OUT/tree/include/avc.h
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Wno-unused-value"
 for s in $SRC/*.hip; do
-  X=""; case $(basename $s) in avc_fused.hip|avc_vc.hip) X="-mllvm --amdgpu-mfma-vgpr-form";; esac
+  X=""; case $(basename $s) in avc_fused.hip|avc_vc.hip) X="-mllvm --amdgpu-mfma-vgpr-form -mllvm -amdgpu-sched-strategy=max-ilp";; esac
   hipcc $F $X -c -o $OUT/$(basename $s .hip).o $s &
 done; wait
 hipcc --offload-arch=gfx950 -shared -o $OUT/libavc.so $OUT/*.o
