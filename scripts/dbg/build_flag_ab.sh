@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../.."
 C=attack-vc_amd/csrc; D=build/ab/$1; mkdir -p $D
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Wno-unused-value -mllvm --amdgpu-mfma-vgpr-form"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Wno-unused-value -mllvm --amdgpu-mfma-vgpr-form"  # + $2 (a -amdgpu-sched-strategy replaces the in-tree max-ilp)
 /opt/rocm/bin/hipcc $F $2 -c $C/avc_fused.hip -o $D/avc_fused.o &
 /opt/rocm/bin/hipcc $F $2 -c $C/avc_vc.hip -o $D/avc_vc.o &
 wait
