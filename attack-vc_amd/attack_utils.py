@@ -19,14 +19,18 @@ Differences from the reference, all documented in DESIGN.md:
     weight gradients, SURVEY.md 8(a) A13);
   * a [B,80,T] batch is B independent attacks by default
     (reduction="independent"); reduction="mean" reproduces the reference called
-    on the batched tensor (its MSE mean over the whole batch).
+    on the batched tensor (its MSE mean over the whole batch);
+  * vc_src, vc_tgt and adv_tgt may have different lengths (attack.py loads each
+    from its own wav), exactly as in the reference;
+  * a module with dropout_rate > 0 in training mode is refused (the reference
+    would apply random dropout inside the loop; see check_no_train_dropout).
 """
 from typing import Optional
 
 import torch
 import torch.nn as nn
 
-from avc_native import context_for, vc_context_for
+from avc_native import check_no_train_dropout, context_for, vc_context_for
 
 
 def _draw_ptb(vc_tgt: torch.Tensor) -> torch.Tensor:
@@ -45,6 +49,7 @@ def emb_attack(model: nn.Module, vc_tgt: torch.Tensor, adv_tgt: torch.Tensor, ep
     Keyword extensions: ptb0 (explicit initial perturbation), reduction,
     precision ("fp32"), return_info (also return {"losses": [n_iters,B],
     "grad0": d loss/d ptb at iteration 0})."""
+    check_no_train_dropout(model.speaker_encoder)
     if ptb0 is None:
         ptb0 = _draw_ptb(vc_tgt)
     ctx = context_for(model.speaker_encoder, vc_tgt.device)

@@ -70,11 +70,22 @@ SIGNATURES = [
     ("avc_emb_attack", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_emb_attack_emb", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
     ("avc_vc_weight_count", ctypes.c_size_t, [ctypes.POINTER(VCCfg)]),
     ("avc_attach_vc", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(VCCfg), ctypes.c_void_p, ctypes.c_size_t]),
     ("avc_vc_out_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_inference", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_inference_emb", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_e2e_attack_emb", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_fb_attack_emb", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                         ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
     ("avc_e2e_attack", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
@@ -194,28 +205,49 @@ class Context:
                                         ctypes.c_void_p(emb.data_ptr()), ctypes.c_void_p(stream)))
         return emb
 
-    def emb_attack(self, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
-                   reduction="independent", use_graph=True, want_losses=False, want_grad0=False):
-        _require_gpu(vc_tgt, adv_tgt, ptb0)
-        vc_tgt, adv_tgt, ptb0 = vc_tgt.contiguous(), adv_tgt.contiguous(), ptb0.contiguous()
-        if vc_tgt.shape != adv_tgt.shape or vc_tgt.shape != ptb0.shape:
-            raise RuntimeError(f"shape mismatch: vc_tgt {tuple(vc_tgt.shape)}, adv_tgt "
-                               f"{tuple(adv_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
-        if vc_tgt.dim() != 3 or vc_tgt.shape[1] != self.cfg["c_in"]:
-            raise RuntimeError(f"expected [B, {self.cfg['c_in']}, T] input, got {tuple(vc_tgt.shape)}")
-        B, C, T = vc_tgt.shape
-        out = torch.empty_like(vc_tgt)
-        losses = torch.empty(n_iters, B, device=vc_tgt.device) if want_losses and n_iters > 0 else None
-        grad0 = torch.empty_like(vc_tgt) if want_grad0 and n_iters > 0 else None
+    @staticmethod
+    def _check_mel(name: str, t: torch.Tensor, c_in: int, B: int = None):
+        if t.dim() != 3 or t.shape[1] != c_in:
+            raise RuntimeError(f"{name}: expected [B, {c_in}, T], got {tuple(t.shape)}")
+        if B is not None and t.shape[0] != B:
+            raise RuntimeError(f"{name}: batch {t.shape[0]} != {B}")
+
+    def _opts(self, precision, reduction, use_graph, n_iters, like, want_losses, want_grad0):
+        B = like.shape[0]
+        losses = torch.empty(n_iters, B, device=like.device) if want_losses and n_iters > 0 else None
+        grad0 = torch.empty_like(like) if want_grad0 and n_iters > 0 else None
         o = AttackOpts(PREC[precision], REDUCE[reduction], 1 if use_graph else 0,
                        losses.data_ptr() if losses is not None else None,
                        grad0.data_ptr() if grad0 is not None else None)
+        return o, losses, grad0
+
+    def emb_attack(self, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
+                   reduction="independent", use_graph=True, want_losses=False, want_grad0=False):
+        """avc_emb_attack; an adv_tgt of another length than vc_tgt is embedded on its own first
+        (the reference embeds it separately, attack_utils.py:74-75) -> avc_emb_attack_emb."""
+        _require_gpu(vc_tgt, adv_tgt, ptb0)
+        vc_tgt, adv_tgt, ptb0 = vc_tgt.contiguous(), adv_tgt.contiguous(), ptb0.contiguous()
+        c_in = self.cfg["c_in"]
+        self._check_mel("vc_tgt", vc_tgt, c_in)
+        B, C, T = vc_tgt.shape
+        self._check_mel("adv_tgt", adv_tgt, c_in, B)
+        if ptb0.shape != vc_tgt.shape:
+            raise RuntimeError(f"shape mismatch: vc_tgt {tuple(vc_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
+        out = torch.empty_like(vc_tgt)
+        o, losses, grad0 = self._opts(precision, reduction, use_graph, n_iters, vc_tgt, want_losses, want_grad0)
         stream = torch.cuda.current_stream(vc_tgt.device).cuda_stream
+        tgt_emb = self.se_forward(adv_tgt) if adv_tgt.shape != vc_tgt.shape else None
         with self._lock:
-            _check(lib().avc_emb_attack(self.h, ctypes.c_void_p(vc_tgt.data_ptr()),
-                                        ctypes.c_void_p(adv_tgt.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()),
-                                        B, T, float(eps), int(n_iters), ctypes.c_void_p(out.data_ptr()),
-                                        ctypes.byref(o), ctypes.c_void_p(stream)))
+            if tgt_emb is None:
+                _check(lib().avc_emb_attack(self.h, ctypes.c_void_p(vc_tgt.data_ptr()),
+                                            ctypes.c_void_p(adv_tgt.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()),
+                                            B, T, float(eps), int(n_iters), ctypes.c_void_p(out.data_ptr()),
+                                            ctypes.byref(o), ctypes.c_void_p(stream)))
+            else:
+                _check(lib().avc_emb_attack_emb(self.h, ctypes.c_void_p(vc_tgt.data_ptr()),
+                                                ctypes.c_void_p(tgt_emb.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()),
+                                                B, T, float(eps), int(n_iters), ctypes.c_void_p(out.data_ptr()),
+                                                ctypes.byref(o), ctypes.c_void_p(stream)))
         return out, losses, grad0
 
     # --- voice-conversion path (ContentEncoder + Decoder) ----------------------------
@@ -236,39 +268,58 @@ class Context:
         return n
 
     def inference(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
+        """AdaInVC.inference: the output takes src's length (models.py:472-489); a tgt of another
+        length is embedded on its own first (avc_inference_emb)."""
         _require_gpu(src, tgt)
         src, tgt = src.contiguous(), tgt.contiguous()
-        if src.shape != tgt.shape or src.dim() != 3:
-            raise RuntimeError(f"inference: src {tuple(src.shape)} and tgt {tuple(tgt.shape)} must be equal [B, 80, T]")
+        c_in = self.cfg["c_in"]
+        self._check_mel("src", src, c_in)
         B, C, T = src.shape
+        self._check_mel("tgt", tgt, c_in, B)
         out = torch.empty(B, 80, self.vc_out_frames(T), device=src.device, dtype=torch.float32)
         stream = torch.cuda.current_stream(src.device).cuda_stream
+        emb = self.se_forward(tgt) if tgt.shape != src.shape else None
         with self._lock:
-            _check(lib().avc_inference(self.h, ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(tgt.data_ptr()),
-                                       B, T, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+            if emb is None:
+                _check(lib().avc_inference(self.h, ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(tgt.data_ptr()),
+                                           B, T, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+            else:
+                _check(lib().avc_inference_emb(self.h, ctypes.c_void_p(src.data_ptr()), B, T,
+                                               ctypes.c_void_p(emb.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                               ctypes.c_void_p(stream)))
         return out
 
     def vc_attack(self, kind: str, vc_src, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
                   reduction="independent", use_graph=True, want_losses=False, want_grad0=False):
-        """kind "e2e" (avc_e2e_attack) or "fb" (avc_fb_attack)."""
+        """kind "e2e" (avc_e2e_attack) or "fb" (avc_fb_attack).  vc_src, vc_tgt and adv_tgt may have
+        different lengths (each is loaded from its own wav by attack.py:49-56): then adv_tgt is
+        embedded on its own and the *_attack_emb entry points run."""
         _require_gpu(vc_src, vc_tgt, adv_tgt, ptb0)
         vc_src, vc_tgt, adv_tgt, ptb0 = (t.contiguous() for t in (vc_src, vc_tgt, adv_tgt, ptb0))
-        if not (vc_src.shape == vc_tgt.shape == adv_tgt.shape == ptb0.shape) or vc_tgt.dim() != 3:
-            raise RuntimeError(f"shape mismatch: vc_src {tuple(vc_src.shape)}, vc_tgt {tuple(vc_tgt.shape)}, "
-                               f"adv_tgt {tuple(adv_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
+        c_in = self.cfg["c_in"]
+        self._check_mel("vc_tgt", vc_tgt, c_in)
         B, C, T = vc_tgt.shape
+        self._check_mel("vc_src", vc_src, c_in, B)
+        self._check_mel("adv_tgt", adv_tgt, c_in, B)
+        if ptb0.shape != vc_tgt.shape:
+            raise RuntimeError(f"shape mismatch: vc_tgt {tuple(vc_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
+        Ts = vc_src.shape[2]
         out = torch.empty_like(vc_tgt)
-        losses = torch.empty(n_iters, B, device=vc_tgt.device) if want_losses and n_iters > 0 else None
-        grad0 = torch.empty_like(vc_tgt) if want_grad0 and n_iters > 0 else None
-        o = AttackOpts(PREC[precision], REDUCE[reduction], 1 if use_graph else 0,
-                       losses.data_ptr() if losses is not None else None,
-                       grad0.data_ptr() if grad0 is not None else None)
-        fn = {"e2e": lib().avc_e2e_attack, "fb": lib().avc_fb_attack}[kind]
+        o, losses, grad0 = self._opts(precision, reduction, use_graph, n_iters, vc_tgt, want_losses, want_grad0)
         stream = torch.cuda.current_stream(vc_tgt.device).cuda_stream
+        same = vc_src.shape == vc_tgt.shape == adv_tgt.shape
+        tgt_emb = None if same else self.se_forward(adv_tgt)
         with self._lock:
-            _check(fn(self.h, ctypes.c_void_p(vc_src.data_ptr()), ctypes.c_void_p(vc_tgt.data_ptr()),
-                      ctypes.c_void_p(adv_tgt.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()), B, T, float(eps),
-                      int(n_iters), ctypes.c_void_p(out.data_ptr()), ctypes.byref(o), ctypes.c_void_p(stream)))
+            if same:
+                fn = {"e2e": lib().avc_e2e_attack, "fb": lib().avc_fb_attack}[kind]
+                _check(fn(self.h, ctypes.c_void_p(vc_src.data_ptr()), ctypes.c_void_p(vc_tgt.data_ptr()),
+                          ctypes.c_void_p(adv_tgt.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()), B, T, float(eps),
+                          int(n_iters), ctypes.c_void_p(out.data_ptr()), ctypes.byref(o), ctypes.c_void_p(stream)))
+            else:
+                fn = {"e2e": lib().avc_e2e_attack_emb, "fb": lib().avc_fb_attack_emb}[kind]
+                _check(fn(self.h, ctypes.c_void_p(vc_src.data_ptr()), Ts, ctypes.c_void_p(vc_tgt.data_ptr()),
+                          ctypes.c_void_p(tgt_emb.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()), B, T, float(eps),
+                          int(n_iters), ctypes.c_void_p(out.data_ptr()), ctypes.byref(o), ctypes.c_void_p(stream)))
         return out, losses, grad0
 
     def set_engine(self, engine: str = "auto"):
@@ -374,15 +425,31 @@ def context_for(se: torch.nn.Module, device: torch.device) -> Context:
     return ctx
 
 
+def check_no_train_dropout(*mods: torch.nn.Module):
+    """The reference never calls .eval() (data_utils.py:219-222, attack.py:38), so a module with
+    dropout_rate > 0 applies random dropout on every forward of its attack loop
+    (models.py:195-204, 298-323, 416-429).  libavc computes the deterministic (eval / p = 0)
+    network only: refuse such a module loudly instead of silently diverging."""
+    for m in mods:
+        d = getattr(m, "dropout_layer", None)
+        if d is not None and float(getattr(d, "p", 0.0)) > 0.0 and m.training:
+            raise NotImplementedError(
+                f"{type(m).__name__} has dropout_rate={d.p} and is in training mode: the reference then applies "
+                "random dropout inside the attack loop (models.py:298-323), which libavc does not reproduce; "
+                "call model.eval() or use dropout_rate=0")
+
+
 def speaker_encoder_forward(se: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
     """SpeakerEncoder.forward (models.py:327-343) on the MI355X; no autograd."""
     _require_gpu(x)
+    check_no_train_dropout(se)
     return context_for(se, x.device).se_forward(x)
 
 
 def vc_context_for(model: torch.nn.Module, device: torch.device) -> Context:
     """Context of model.speaker_encoder with model.content_encoder / model.decoder attached
     (re-attached whenever their parameters change)."""
+    check_no_train_dropout(model.speaker_encoder, model.content_encoder, model.decoder)
     ctx = context_for(model.speaker_encoder, device)
     mods = (model.content_encoder, model.decoder)
     version = tuple((p.data_ptr(), p._version) for m in mods for p in m.parameters())

@@ -172,6 +172,12 @@ struct avc_ctx {
     std::map<const float*, void*> bf16_of;   // fp32 A matrix -> its bf16 copy (device)
     hipStream_t stream = nullptr;
     hipEvent_t ev_user = nullptr, ev_done = nullptr;
+    // per-call constants (Adam table, scalars) go through this persistent pinned buffer:
+    // the copies stay asynchronous, and a later call only waits for them (ev_stage), never
+    // for the caller's queued work
+    float* stage = nullptr;
+    size_t stage_n = 0;
+    hipEvent_t ev_stage = nullptr;
     Workspace ws;
     bool profiling = false;
     std::map<std::string, std::pair<double, double>> prof;   // name -> (total ms, total flop)
@@ -290,7 +296,11 @@ static size_t weight_count(const avc_se_cfg& c) {
 
 extern "C" size_t avc_se_weight_count(const avc_se_cfg* cfg) { return cfg ? weight_count(*cfg) : 0; }
 extern "C" const char* avc_last_error(void) { return g_err.c_str(); }
-extern "C" const char* avc_version(void) { return "libavc 0.1 (gfx950, fp32 MFMA)"; }
+#ifndef AVC_SRC_HASH
+#define AVC_SRC_HASH "unknown"
+#endif
+// "src=<hash>": __graft_entry__.source_hash() of the sources this library was built from
+extern "C" const char* avc_version(void) { return "libavc 0.2 (gfx950) src=" AVC_SRC_HASH; }
 
 static int validate_cfg(const avc_se_cfg& c) {
     if (c.c_in <= 0 || c.c_h <= 0 || c.c_out <= 0 || c.c_bank <= 0) return fail("bad channel counts");
@@ -630,6 +640,7 @@ extern "C" int avc_create(int device, const avc_se_cfg* cfgp, const float* w, si
     hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_user, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_stage, hipEventDisableTiming);
     if (e == hipSuccess) {
         const int S = c.c_h > c.c_out ? c.c_h : c.c_out;
         const size_t lds = (size_t)(2 * nd + 5) * S * 16 * sizeof(float);
@@ -697,6 +708,8 @@ extern "C" void avc_destroy(avc_ctx* ctx) {
     ctx->bf16_of.clear();
     if (ctx->ev_user) hipEventDestroy(ctx->ev_user);
     if (ctx->ev_done) hipEventDestroy(ctx->ev_done);
+    if (ctx->ev_stage) hipEventDestroy(ctx->ev_stage);
+    if (ctx->stage) (void)hipHostFree(ctx->stage);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1594,10 +1607,41 @@ extern "C" int avc_set_profiling(avc_ctx* ctx, int enable) {
     return 0;
 }
 
-extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* ptb0, int B,
-                              int T, float eps, int n_iters, float* out_adv, const avc_attack_opts* opts,
-                              void* stream) {
-    if (!ctx || !vc_tgt || !adv_tgt || !ptb0 || !out_adv) return fail("avc_emb_attack: null argument");
+// Adam scalars per step (computed in double like torch's Python-side math) and the per-call
+// scalars [eps, loss-grad scales...] -> ws.table / ws.scal on ctx->stream, asynchronously
+// through the pinned staging buffer
+static int stage_call_consts(avc_ctx* ctx, int n_iters, const float scal[4]) {
+    Workspace& ws = ctx->ws;
+    const size_t nt = 2 * (size_t)std::max(n_iters, 1);
+    HIPCHK(hipEventSynchronize(ctx->ev_stage));   // the previous call's staging copies are done
+    if (ctx->stage_n < nt + 4) {
+        if (ctx->stage) (void)hipHostFree(ctx->stage);
+        ctx->stage = nullptr;
+        ctx->stage_n = 0;
+        HIPCHK(hipHostMalloc((void**)&ctx->stage, (nt + 4) * sizeof(float), hipHostMallocDefault));
+        ctx->stage_n = nt + 4;
+    }
+    float* table = ctx->stage;
+    for (size_t i = 0; i < nt; ++i) table[i] = 0.f;
+    for (int t = 1; t <= n_iters; ++t) {
+        const double bc1 = 1.0 - std::pow(0.9, t);
+        const double bc2 = 1.0 - std::pow(0.999, t);
+        table[2 * (t - 1)] = (float)(-(1e-3 / bc1));
+        table[2 * (t - 1) + 1] = (float)std::sqrt(bc2);
+    }
+    for (int i = 0; i < 4; ++i) table[nt + i] = scal[i];
+    HIPCHK(hipMemcpyAsync(ws.table.p, table, nt * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ws.scal.p, table + nt, 4 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_stage, ctx->stream));
+    return 0;
+}
+
+// emb attack; the target embedding is SE(adv_tgt) at T frames (adv_tgt given) or the caller's
+// tgt_emb [B][c_out] (adv_tgt of another length, embedded beforehand by avc_se_forward)
+static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* tgt_emb,
+                           const float* ptb0, int B, int T, float eps, int n_iters, float* out_adv,
+                           const avc_attack_opts* opts, void* stream) {
+    if (!ctx || !vc_tgt || !(adv_tgt || tgt_emb) || !ptb0 || !out_adv) return fail("avc_emb_attack: null argument");
     if (n_iters < 0) return fail("n_iters must be >= 0");
     avc_attack_opts o{};
     o.use_graph = 1;
@@ -1610,6 +1654,9 @@ extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* ad
     Workspace& ws = ctx->ws;
     const bool bf16 = o.precision == AVC_PREC_BF16;
     if (bf16 && ws.iter_bf16.launches.empty()) {
+        // the setup below rewrites eps and the step counter with blocking copies on the null
+        // stream: an earlier (asynchronous) call's loop on ctx->stream must be finished first
+        HIPCHK(hipStreamSynchronize(ctx->stream));
         if (plan_iteration(ctx, ws, ws.iter_bf16, PREC_BF16)) return 1;
         const float scal0[4] = {0.1f, 0.f, 0.f, 0.f};
         HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
@@ -1623,29 +1670,20 @@ extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* ad
     const size_t X = (size_t)B * c.c_in * T;
     const float gscale = (float)(2.0 / (o.reduction == AVC_REDUCE_MEAN ? (double)B * c.c_out : (double)c.c_out));
 
-    // Adam scalars per step, computed in double like torch's Python-side math
-    std::vector<float> table(2 * (size_t)std::max(n_iters, 1));
-    for (int t = 1; t <= n_iters; ++t) {
-        const double bc1 = 1.0 - std::pow(0.9, t);
-        const double bc2 = 1.0 - std::pow(0.999, t);
-        table[2 * (t - 1)] = (float)(-(1e-3 / bc1));
-        table[2 * (t - 1) + 1] = (float)std::sqrt(bc2);
-    }
-    HIPCHK(hipMemcpyAsync(ws.table.p, table.data(), table.size() * sizeof(float), hipMemcpyHostToDevice,
-                          ctx->stream));
     const float scal[4] = {eps, gscale, 0.f, 0.f};
-    HIPCHK(hipMemcpyAsync(ws.scal.p, scal, sizeof(scal), hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));   // host staging buffers above are stack/heap locals
+    if (stage_call_consts(ctx, n_iters, scal)) return 1;
     HIPCHK(hipMemcpyAsync(ws.vc.p, vc_tgt, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     // org_emb = SE(vc_tgt), tgt_emb = SE(adv_tgt)   (attack_utils.py:73-75)
     HIPCHK(hipMemcpyAsync(ws.xin.p, vc_tgt, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     if (run_plan(ctx, ws.fwd, false)) return 1;
     HIPCHK(hipMemcpyAsync(ws.org.p, ws.emb_fwd.p, (size_t)B * c.c_out * sizeof(float), hipMemcpyDeviceToDevice,
                           ctx->stream));
-    HIPCHK(hipMemcpyAsync(ws.xin.p, adv_tgt, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
-    if (run_plan(ctx, ws.fwd, false)) return 1;
-    HIPCHK(hipMemcpyAsync(ws.tgt.p, ws.emb_fwd.p, (size_t)B * c.c_out * sizeof(float), hipMemcpyDeviceToDevice,
-                          ctx->stream));
+    if (adv_tgt) {
+        HIPCHK(hipMemcpyAsync(ws.xin.p, adv_tgt, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+        if (run_plan(ctx, ws.fwd, false)) return 1;
+    }
+    HIPCHK(hipMemcpyAsync(ws.tgt.p, adv_tgt ? ws.emb_fwd.p : tgt_emb, (size_t)B * c.c_out * sizeof(float),
+                          hipMemcpyDeviceToDevice, ctx->stream));
     // ptb <- ptb0, Adam state 0, adv = vc + eps*tanh(ptb)
     hipLaunchKernelGGL(attack_init, dim3((unsigned)((X + 255) / 256)), dim3(256), 0, ctx->stream, ws.vc.p, ptb0,
                        ws.ptb.p, ws.m.p, ws.v.p, ws.adv.p, eps, X);
@@ -1694,6 +1732,20 @@ extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* ad
     if (o.grad0 && n_iters > 0)
         HIPCHK(hipMemcpyAsync(o.grad0, ws.grad0.p, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     return end_call(ctx, us);
+}
+
+extern "C" int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* ptb0, int B,
+                              int T, float eps, int n_iters, float* out_adv, const avc_attack_opts* opts,
+                              void* stream) {
+    if (!adv_tgt) return fail("avc_emb_attack: null argument");
+    return emb_attack_impl(ctx, vc_tgt, adv_tgt, nullptr, ptb0, B, T, eps, n_iters, out_adv, opts, stream);
+}
+
+extern "C" int avc_emb_attack_emb(avc_ctx* ctx, const float* vc_tgt, const float* tgt_emb, const float* ptb0, int B,
+                                  int T, float eps, int n_iters, float* out_adv, const avc_attack_opts* opts,
+                                  void* stream) {
+    if (!tgt_emb) return fail("avc_emb_attack_emb: null argument");
+    return emb_attack_impl(ctx, vc_tgt, nullptr, tgt_emb, ptb0, B, T, eps, n_iters, out_adv, opts, stream);
 }
 
 extern "C" int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_flop_per_iter) {

@@ -32,7 +32,14 @@
         }                                                                          \
     } while (0)
 
+#ifndef AVC_SRC_HASH
+#define AVC_SRC_HASH "unknown"
+#endif
+// the sources this driver was built with (a stale libavc.so next to it shows up in the log)
+static const char* const kBuiltFrom = "src=" AVC_SRC_HASH;
+
 int main(int argc, char** argv) {
+    fprintf(stderr, "avc_bench %s; %s\n", kBuiltFrom, avc_version());
     const int B = argc > 1 ? atoi(argv[1]) : 256;
     const int T = argc > 2 ? atoi(argv[2]) : 128;
     const int n_iters = argc > 3 ? atoi(argv[3]) : 1500;

@@ -948,14 +948,27 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 p[e] = p[e] + nstep * (mm[e] * (vv[e] * bc2s + Ad.adam_eps));
                 ad[e] = X[k][e] + eps * p[e] * 0.25f;
 #else
-                const float th = fast_tanh(p[e]);
-                g[e] = (gsum[e] * eps) * (1.f - th * th);
-                mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
-                vv[e] = vv[e] * Ad.b2;
-                vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
-                const float den = __builtin_amdgcn_sqrtf(vv[e]) * rbc2s + Ad.adam_eps;
-                p[e] = p[e] + nstep * (mm[e] * __builtin_amdgcn_rcpf(den));
-                ad[e] = X[k][e] + eps * fast_tanh(p[e]);
+                if constexpr (PREC == PREC_F32) {
+                    // fp32 mode: torch's IEEE arithmetic (tanh, sqrt(v) / sqrt(bc2) + eps, m / den;
+                    // _single_tensor_adam, torch/optim/adam.py:531-547)
+                    const float th = tanhf(p[e]);
+                    g[e] = (gsum[e] * eps) * (1.f - th * th);
+                    mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
+                    vv[e] = vv[e] * Ad.b2;
+                    vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
+                    p[e] = p[e] + nstep * (mm[e] / (sqrtf(vv[e]) / bc2s + Ad.adam_eps));
+                    ad[e] = X[k][e] + eps * tanhf(p[e]);
+                } else {
+                    // bf16 mode: hardware exp2 / rcp / sqrt (the tail is VALU-bound at one wave per SIMD)
+                    const float th = fast_tanh(p[e]);
+                    g[e] = (gsum[e] * eps) * (1.f - th * th);
+                    mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
+                    vv[e] = vv[e] * Ad.b2;
+                    vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
+                    const float den = __builtin_amdgcn_sqrtf(vv[e]) * rbc2s + Ad.adam_eps;
+                    p[e] = p[e] + nstep * (mm[e] * __builtin_amdgcn_rcpf(den));
+                    ad[e] = X[k][e] + eps * fast_tanh(p[e]);
+                }
 #endif
             }
             if (g04) g04[q] = g;

@@ -426,11 +426,12 @@ struct MaskRd {
     }
 };
 
-// tanh for the Adam tail (attack_utils.py:77-78,86: eps * tanh(ptb)) on the hardware
-// exp2 / reciprocal instead of the libm sequence (the tail was VALU-bound on it: 2
-// tanh + sqrt + 2 IEEE divisions per element at one wave per SIMD).  |x| < 0.625: odd
+// tanh for the bf16 mode's Adam tail (attack_utils.py:77-78,86: eps * tanh(ptb)) on the
+// hardware exp2 / reciprocal instead of the libm sequence (the tail was VALU-bound on it:
+// 2 tanh + sqrt + 2 IEEE divisions per element at one wave per SIMD).  |x| < 0.625: odd
 // polynomial x + x^3 P(x^2) (least-squares fit in relative error, <= 0.9 ulp in f32);
-// otherwise 1 - 2 / (1 + e^{2|x|}) (<= 2 ulp).  Parity: tests/test_gpu_*.py tolerances.
+// otherwise 1 - 2 / (1 + e^{2|x|}) (<= 2 ulp).  The fp32 mode keeps tanhf / sqrtf / IEEE
+// division (torch's arithmetic).  Parity: tests/test_gpu_*.py tolerances.
 __device__ __forceinline__ float fast_tanh(float x) {
     const float a = __builtin_fabsf(x);
     const float x2 = x * x;

@@ -127,9 +127,12 @@ def read_wav(path: str) -> Tuple[np.ndarray, int]:
 
 def write_wav(path: str, wav: np.ndarray, sample_rate: int) -> None:
     """soundfile.write(path, wav, sr) for a .wav path: 16-bit PCM (soundfile's default
-    subtype), samples clipped to [-1, 1)."""
-    x = np.clip(np.asarray(wav, np.float64), -1.0, 1.0 - 1.0 / 32768)
-    pcm = np.round(x * 32768.0).astype("<i2")
+    subtype) with libsndfile's float -> PCM_16 conversion: lrintf(x * 0x7FFF) (round half to
+    even).  libsndfile does not clip by default (out-of-range samples overflow the short);
+    here they saturate at -32768 / 32767 instead -- the only difference (parity unpinned: no
+    soundfile output exists in the reference)."""
+    x = np.rint(np.asarray(wav, np.float64) * 32767.0)
+    pcm = np.clip(x, -32768, 32767).astype("<i2")
     with wave.open(path, "wb") as w:
         w.setnchannels(1)
         w.setsampwidth(2)

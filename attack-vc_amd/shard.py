@@ -7,9 +7,9 @@ Two drivers:
   * one process per GPU (torchrun; bench.py): `shard_slice` picks the rank's
     utterances, `max_over_ranks` / `gather_shards` are the only collectives
     (timing and the final host-side gather);
-  * one process, several GPUs (`emb_attack_multi_gpu`): one host thread per
-    device, each with its own libavc context and stream, results gathered on
-    the first device.
+  * one process, several GPUs (`attack_multi_gpu`, emb / e2e / fb): one host
+    thread per device, each with its own libavc context and stream, results
+    gathered on the first device.
 """
 import threading
 from typing import List, Optional, Sequence
@@ -49,20 +49,27 @@ def gather_shards(shard: torch.Tensor, total: int, dist=None) -> torch.Tensor:
     return torch.cat([o[:n] for o, n in zip(outs, sizes)], dim=0)
 
 
-def emb_attack_multi_gpu(model_per_device: Sequence[torch.nn.Module], vc_tgt: torch.Tensor, adv_tgt: torch.Tensor,
-                         eps: float, n_iters: int, ptb0: Optional[torch.Tensor] = None,
-                         precision: str = "fp32") -> torch.Tensor:
-    """emb_attack over len(model_per_device) GPUs from one process.
+def attack_multi_gpu(kind: str, model_per_device: Sequence[torch.nn.Module], vc_src: Optional[torch.Tensor],
+                     vc_tgt: torch.Tensor, adv_tgt: torch.Tensor, eps: float, n_iters: int,
+                     ptb0: Optional[torch.Tensor] = None, precision: str = "fp32") -> torch.Tensor:
+    """emb / e2e / fb attack (attack_utils.py:51-86 / 7-48 / 89-130) over len(model_per_device)
+    GPUs from one process: one host thread per device, each attacking a contiguous utterance
+    shard with its own libavc context and stream; the results are gathered on the first
+    device.  model_per_device[i] must live on its own device; inputs may live anywhere.
+    Utterance b of the result equals a single-GPU attack of utterance b (the shards share
+    nothing).  This is configs[3]'s path (fb, B = 2048 over 8 GPUs) without torchrun."""
+    import attack_utils
 
-    model_per_device[i] must live on its own device; inputs may live anywhere.
-    Utterance b of the result equals a single-GPU attack of utterance b (the
-    shards share nothing)."""
-    from attack_utils import emb_attack
-
+    if kind not in ("emb", "e2e", "fb"):
+        raise ValueError(f"unknown attack {kind!r}")
+    if kind != "emb" and vc_src is None:
+        raise ValueError("e2e / fb attacks need vc_src")
     devs = [next(m.parameters()).device for m in model_per_device]
     B = vc_tgt.shape[0]
     if ptb0 is None:
-        ptb0 = torch.zeros_like(vc_tgt).normal_(0, 1)
+        # drawn on the first model's device, as the reference draws it on the attack's device
+        # (attack_utils.py:68): a seeded caller gets the single-GPU perturbation bit for bit
+        ptb0 = torch.zeros(vc_tgt.shape, dtype=torch.float32, device=devs[0]).normal_(0, 1)
     outs: List[Optional[torch.Tensor]] = [None] * len(devs)
     errs: List[BaseException] = []
 
@@ -73,8 +80,13 @@ def emb_attack_multi_gpu(model_per_device: Sequence[torch.nn.Module], vc_tgt: to
                 return
             d = devs[i]
             with torch.cuda.device(d):
-                o = emb_attack(model_per_device[i], vc_tgt[sl].to(d), adv_tgt[sl].to(d), eps, n_iters,
-                               ptb0=ptb0[sl].to(d), precision=precision)
+                if kind == "emb":
+                    o = attack_utils.emb_attack(model_per_device[i], vc_tgt[sl].to(d), adv_tgt[sl].to(d), eps,
+                                                n_iters, ptb0=ptb0[sl].to(d), precision=precision)
+                else:
+                    fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
+                    o = fn(model_per_device[i], vc_src[sl].to(d), vc_tgt[sl].to(d), adv_tgt[sl].to(d), eps, n_iters,
+                           ptb0=ptb0[sl].to(d), precision=precision)
                 torch.cuda.current_stream(d).synchronize()
             outs[i] = o.detach()
         except BaseException as e:  # re-raised on the calling thread
@@ -88,3 +100,10 @@ def emb_attack_multi_gpu(model_per_device: Sequence[torch.nn.Module], vc_tgt: to
     if errs:
         raise errs[0]
     return torch.cat([o.to(devs[0]) for o in outs if o is not None], dim=0).requires_grad_(True)
+
+
+def emb_attack_multi_gpu(model_per_device: Sequence[torch.nn.Module], vc_tgt: torch.Tensor, adv_tgt: torch.Tensor,
+                         eps: float, n_iters: int, ptb0: Optional[torch.Tensor] = None,
+                         precision: str = "fp32") -> torch.Tensor:
+    """emb_attack over len(model_per_device) GPUs from one process (attack_multi_gpu)."""
+    return attack_multi_gpu("emb", model_per_device, None, vc_tgt, adv_tgt, eps, n_iters, ptb0, precision)

@@ -9,9 +9,13 @@ mel2wav (inverse dB, inv_mel_matrix, 100 Griffin-Lim iterations, de-emphasis) of
 80x128 mels per GPU, vocoded utts/s.
 
 One "step" = one complete 1500-iteration attack over the rank's batch
-(inputs already resident in HBM).  N>1: one process per GPU (torchrun), each
-rank attacks its own contiguous shard of the global batch (no data-path
-collective; scaling "weak"), barrier + max-over-ranks timing.
+(inputs already resident in HBM).  N>1: one process per GPU, each rank attacks its
+own contiguous shard of the global batch (no data-path collective; scaling "weak"),
+barrier + max-over-ranks timing.  Under torchrun the ranks come from the environment;
+`python bench.py --gpus N` without it launches the N rank processes itself (and fails
+loudly when fewer than N GPUs are visible -- never a silent 1-GPU run).  --dry-run
+exercises that launcher, the rendezvous (gloo), sharding, timing and the JSON line on
+the CPU without computing an attack (the multi-rank CPU test drives it).
 
 Also reported:
   roofline      dominant kernel's algorithmic FLOP / its average launch time
@@ -74,15 +78,81 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="CPU baseline (ii): concurrent 1-thread processes (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-worker", type=float, default=0.0, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: launcher + gloo rendezvous + sharding + timing, no attack computed")
     return ap.parse_args()
 
 
-def cpu_baseline(model, budget_s, kind="emb"):
-    """Reference attack loop (torch CPU, B=1, all host threads used by ATen)."""
+def launch_ranks(a) -> int:
+    """--gpus N without torchrun: start N rank processes of this script (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set like torchrun, 127.0.0.1 rendezvous) and return the worst exit
+    code.  Runs before anything touches the GPU in this process (device_count() does not)."""
+    import socket
+    import subprocess
+    if not a.dry_run:
+        n = torch.cuda.device_count()
+        if n < a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} requested but only {n} GPU(s) are visible; "
+                             f"refusing to report a {n}-GPU number as {a.gpus}")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
+
+
+def main_dry_run(a):
+    """The multi-rank path of main() on the CPU: gloo rendezvous, the rank's contiguous shard,
+    barrier-bracketed timing, max over ranks, one JSON line from rank 0.  The "step" only
+    touches the shard (no attack): this checks the orchestration, not the kernels."""
+    import torch.distributed as dist_mod
+    import shard
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist = None
+    if world > 1:
+        dist = dist_mod
+        dist.init_process_group("gloo")
+    total = a.batch * world
+    sl = shard.shard_slice(total, rank, world)
+    vc = torch.randn(total, 80, a.frames, generator=torch.Generator().manual_seed(1))[sl]
+    for _ in range(a.warmup):
+        vc.sum()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        s = vc.double().sum()
+    if dist:
+        dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, None)
+    sizes = torch.tensor([sl.stop - sl.start], dtype=torch.int64)
+    if dist:
+        allz = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allz, sizes)
+        sizes = torch.cat(allz)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "shard_sizes": [int(x) for x in sizes], "global_batch": total,
+                          "value": round(total * a.steps / max(elapsed, 1e-9), 3), "checksum": float(s)}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def _cpu_sample(model_sd, kind, budget_s, threads):
+    """Time the reference loop (B=1, 80x128) for about budget_s seconds; returns
+    (iterations timed, seconds per iteration)."""
     from oracle import torch_cpu
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    sd = model_sd
     g = torch.Generator().manual_seed(1)
     vc, at = torch.randn(1, 80, 128, generator=g), torch.randn(1, 80, 128, generator=g)
     p0 = torch.randn(1, 80, 128, generator=torch.Generator().manual_seed(123))
@@ -106,11 +176,54 @@ def cpu_baseline(model, budget_s, kind="emb"):
         run(1500, hook)
     except StopIteration:
         pass
-    n = len(stamps)
-    per_iter = (stamps[-1] - t0) / n
-    return {"value": 1.0 / (per_iter * 1500), "unit": "utts/s", "cores": threads, "kind": "port",
-            "sample": f"B=1 {kind}_attack 80x128, {n} of 1500 iterations timed ({per_iter*1e3:.2f} ms/iter), "
-                      f"scaled x1500; oracle/torch_cpu.py (reference ATen arithmetic incl. weight grads)"}
+    return len(stamps), (stamps[-1] - t0) / len(stamps)
+
+
+def cpu_worker(a):
+    """--cpu-worker SECONDS: one 1-thread process of CPU baseline (ii); prints its sample."""
+    import models
+    torch.manual_seed(0)
+    model = models.AdaInVC(FULL_CFG)
+    n, per_iter = _cpu_sample({k: v.detach().cpu() for k, v in model.state_dict().items()}, a.attack, a.cpu_worker, 1)
+    print(json.dumps({"iters": n, "per_iter": per_iter}), flush=True)
+
+
+def cpu_baseline_throughput(kind, budget_s, procs):
+    """BASELINE.md CPU baseline (ii): `procs` concurrent 1-thread processes, B=1 each (the
+    throughput a CPU box gets from the reference), aggregated utts/s.  Child processes of
+    this script (--cpu-worker), started with subprocess."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.abspath(__file__), "--attack", kind, "--cpu-worker", str(budget_s)]
+    ps = [subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, env=env)
+          for _ in range(procs)]
+    per = []
+    for p in ps:
+        out, _ = p.communicate(timeout=budget_s * 4 + 180)
+        lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+        if p.returncode == 0 and lines:
+            per.append(json.loads(lines[-1])["per_iter"])
+    if not per:
+        return None
+    agg = sum(1.0 / (t * 1500) for t in per)
+    return {"value": round(agg, 4), "unit": "utts/s", "cores": len(per), "kind": "port",
+            "sample": f"{len(per)} concurrent 1-thread processes, B=1 {kind}_attack 80x128 each, ~{budget_s:.0f} s "
+                      f"of iterations timed per process ({1e3 * min(per):.1f}-{1e3 * max(per):.1f} ms/iter), "
+                      f"scaled x1500 and summed"}
+
+
+def cpu_baseline(model, budget_s, kind="emb", procs=16):
+    """Reference attack loop on the host: (i) as shipped -- one process, B=1, all host threads
+    used by ATen -- and (ii) throughput -- `procs` concurrent 1-thread processes."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    n, per_iter = _cpu_sample({k: v.detach().cpu() for k, v in model.state_dict().items()}, kind, budget_s, threads)
+    out = {"value": 1.0 / (per_iter * 1500), "unit": "utts/s", "cores": threads, "kind": "port",
+           "sample": f"B=1 {kind}_attack 80x128, {n} of 1500 iterations timed ({per_iter*1e3:.2f} ms/iter), "
+                     f"scaled x1500; oracle/torch_cpu.py (reference ATen arithmetic incl. weight grads)"}
+    if procs > 0:
+        out["throughput"] = cpu_baseline_throughput(kind, min(budget_s, 15.0), procs)
+    return out
 
 
 def cpu_baseline_pm(budget_s, sd):
@@ -307,6 +420,12 @@ def main_mel2wav(a):
 
 def main():
     a = parse()
+    if a.cpu_worker > 0:
+        return cpu_worker(a)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(a))
+    if a.dry_run:
+        return main_dry_run(a)
     if a.attack == "pm":
         return main_pm(a)
     if a.attack == "mel2wav":
@@ -314,7 +433,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world > 1:
+    if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -412,7 +531,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(model, a.cpu_seconds, a.attack)
+        cpu = cpu_baseline(model, a.cpu_seconds, a.attack, a.cpu_procs)
 
     if rank == 0:
         ms = elapsed / a.steps * 1e3
@@ -431,6 +550,7 @@ def main():
                        "batch_per_gpu": B, "frames": T, "n_iters": a.n_iters, "eps": a.eps,
                        "parallelism": f"dp{world} (independent utterance shards, no collective)"},
             "roofline": roof, "cpu_baseline": cpu, "fp32": fp32_cmp,
+            "libavc": avc_native.lib().avc_version().decode(),
             "flop_per_utt_iter": fl,
             "tflops_whole_step": round(fl * a.n_iters * total * a.steps / elapsed / 1e12, 2),
         }

@@ -5,6 +5,9 @@
  * This is the boundary behind the reference's Python attack functions:
  *
  *   avc_emb_attack   replaces  attack_utils.emb_attack   (/root/reference/attack_utils.py:51-86)
+ *   avc_*_attack_emb the same with adv_tgt embedded beforehand (an adv_tgt of another length:
+ *                    attack_utils.py:74-75 / 117-119 embed it on its own, attack.py:49-56 loads
+ *                    each input from its own wav)
  *   avc_se_forward   replaces  SpeakerEncoder.forward    (/root/reference/models.py:327-343)
  *   avc_create       replaces  AdaInVC(config) + load_state_dict of the speaker encoder
  *                              (/root/reference/data_utils.py:219-221, models.py:213-283)
@@ -100,6 +103,13 @@ int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, cons
                    int B, int T, float eps, int n_iters, float* out_adv,
                    const avc_attack_opts* opts, void* stream);
 
+/* The same attack with the target embedding given: tgt_emb [B, c_out] device fp32 =
+ * SpeakerEncoder(adv_tgt) for an adv_tgt of any length (avc_se_forward).  The reference embeds
+ * adv_tgt on its own (attack_utils.py:74-75), so its length never has to match vc_tgt's. */
+int avc_emb_attack_emb(avc_ctx* ctx, const float* vc_tgt, const float* tgt_emb, const float* ptb0,
+                       int B, int T, float eps, int n_iters, float* out_adv,
+                       const avc_attack_opts* opts, void* stream);
+
 /* ---- voice-conversion path: ContentEncoder + Decoder (e2e / feedback attacks) ----
  * ContentEncoder / Decoder hyper-parameters, config.yaml model.ContentEncoder /
  * model.Decoder (/root/reference/models.py:121-208, 346-435).  act: 0 = ReLU, 1 = LeakyReLU. */
@@ -132,6 +142,11 @@ int avc_vc_out_frames(avc_ctx* ctx, int T);
  * SpeakerEncoder(tgt))  (models.py:472-489); src, tgt [B, 80, T]; fp32. */
 int avc_inference(avc_ctx* ctx, const float* src, const float* tgt, int B, int T, float* out, void* stream);
 
+/* out[B, 80, Tn(T_src)] = Decoder(ContentEncoder(src).mu, emb): src [B, 80, T_src], emb [B, c_out]
+ * = SpeakerEncoder(tgt) for a tgt of any length (avc_se_forward). */
+int avc_inference_emb(avc_ctx* ctx, const float* src, int B, int T_src, const float* emb, float* out,
+                      void* stream);
+
 /* End-to-end attack (attack_utils.py:7-48) and feedback attack (attack_utils.py:89-130):
  * same buffers and options as avc_emb_attack plus vc_src [B, c_in, T].  losses (optional)
  * [n_iters, B]: e2e MSE(dec, tgt_out) - 0.1 MSE(dec, org_out); fb MSE(SE(dec), tgt_emb) -
@@ -142,6 +157,17 @@ int avc_e2e_attack(avc_ctx* ctx, const float* vc_src, const float* vc_tgt, const
 int avc_fb_attack(avc_ctx* ctx, const float* vc_src, const float* vc_tgt, const float* adv_tgt,
                   const float* ptb0, int B, int T, float eps, int n_iters, float* out_adv,
                   const avc_attack_opts* opts, void* stream);
+
+/* e2e / feedback attacks with independent lengths: vc_src [B, c_in, T_src]; vc_tgt, ptb0 and
+ * out_adv [B, c_in, T]; tgt_emb [B, c_out] = SpeakerEncoder(adv_tgt) (any adv_tgt length).
+ * The decoder output (and the e2e objective) has Tn(T_src) frames, as in the reference, where
+ * inference(vc_src, .) takes its length from vc_src (models.py:472-489). */
+int avc_e2e_attack_emb(avc_ctx* ctx, const float* vc_src, int T_src, const float* vc_tgt,
+                       const float* tgt_emb, const float* ptb0, int B, int T, float eps, int n_iters,
+                       float* out_adv, const avc_attack_opts* opts, void* stream);
+int avc_fb_attack_emb(avc_ctx* ctx, const float* vc_src, int T_src, const float* vc_tgt,
+                      const float* tgt_emb, const float* ptb0, int B, int T, float eps, int n_iters,
+                      float* out_adv, const avc_attack_opts* opts, void* stream);
 
 /* ---- VSMask PredictiveModel forward (models/predictive_model.py:53-110, BASELINE config 5) ----
  * Eval-mode inference (BatchNorm running statistics).  `weights` = HOST fp32 floating

@@ -84,3 +84,36 @@ def test_gloo_two_ranks_gather_and_max(total):
     ref = np.concatenate([oracle.se_forward(w, cfg["SpeakerEncoder"], x[b:b + 1])[0] for b in range(total)])
     assert np.array_equal(full, ref)
     assert t == 2.0
+
+
+def _bench(*args, timeout=240):
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + list(args), capture_output=True,
+                          text=True, timeout=timeout, env=env)
+
+
+@pytest.mark.parametrize("world,batch", [(2, 8), (3, 5)])
+def test_bench_launcher_dry_run(world, batch):
+    """`python bench.py --gpus N` without torchrun starts the N rank processes itself (gloo
+    here: --dry-run computes no attack); rank 0 prints one JSON line whose shards cover the
+    global batch exactly."""
+    import json
+    r = _bench("--gpus", str(world), "--dry-run", "--batch", str(batch), "--frames", "16", "--steps", "2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["global_batch"] == batch * world
+    assert out["shard_sizes"] == [batch] * world
+
+
+def test_bench_refuses_missing_gpus():
+    """No silent single-GPU number: --gpus 2 with fewer visible GPUs (none here) fails loudly."""
+    r = _bench("--gpus", "2", "--steps", "1", timeout=120)
+    assert r.returncode != 0
+    assert "GPU(s) are visible" in (r.stderr + r.stdout)

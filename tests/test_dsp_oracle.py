@@ -132,7 +132,9 @@ def test_wav_io_roundtrip(tmp_path):
     data_utils.write_wav(p, x, 16000)
     y, sr = data_utils.read_wav(p)
     assert sr == 16000 and len(y) == len(x)
-    assert np.abs(y - np.clip(x, -1, 1 - 1 / 32768)).max() <= 0.5 / 32768 + 1e-7
+    # libsndfile's float -> PCM_16 (lrintf(x * 0x7FFF)), saturated; read back as PCM / 32768
+    want = np.clip(np.rint(x.astype(np.float64) * 32767.0), -32768, 32767) / 32768.0
+    assert np.array_equal(y, want.astype(np.float32))
     # resampling on load (librosa.load(sr=...))
     z = data_utils.load_wav(p, 8000)
     assert abs(len(z) - 1500) <= 1

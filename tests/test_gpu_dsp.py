@@ -188,7 +188,9 @@ def test_file2mel_mel2wav_roundtrip(tmp_path):
 
 
 def test_attack_cli_end_to_end(tmp_path, golden):
-    """attack.py main() (the reference's CLI): wav files in, defended wav out, all on the GPU."""
+    """attack.py main() (the reference's CLI): wav files in, defended wav out, all on the GPU.
+    The three wavs have different lengths, as real utterances do (attack.py:49-56 loads each
+    on its own; the reference's attacks never require equal lengths)."""
     import pickle
 
     import yaml
@@ -206,14 +208,17 @@ def test_attack_cli_end_to_end(tmp_path, golden):
     with open(d / "attr.pkl", "wb") as f:
         pickle.dump({"mean": np.full(80, 0.4), "std": np.full(80, 0.2)}, f)
     paths = {}
+    frames = {"src": 90, "tgt": 110, "adv": 70}
     for i, k in enumerate(("src", "tgt", "adv")):
         paths[k] = str(tmp_path / f"{k}.wav")
-        data_utils.write_wav(paths[k], _signal(300 * 100, 16000, 20 + i), 16000)
-    for kind in ("emb", "e2e"):
+        data_utils.write_wav(paths[k], _signal(300 * frames[k], 16000, 20 + i), 16000)
+    n_tgt = data_utils.file2mel(paths["tgt"], **pre).shape[0]
+    for kind in ("emb", "e2e", "fb"):
         out = str(tmp_path / f"out_{kind}.wav")
         attack.main(str(d), paths["src"], paths["tgt"], paths["adv"], out, 0.1, 5, kind)
         w, sr = data_utils.read_wav(out)
-        assert sr == 16000 and len(w) > 16000 and np.isfinite(w).all()
+        # the defended utterance keeps vc_tgt's frames (mel2wav: hop * (T - 1) samples)
+        assert sr == 16000 and len(w) == pre["hop_length"] * (n_tgt - 1) and np.isfinite(w).all()
 
 
 def test_deemphasis_long_signal():

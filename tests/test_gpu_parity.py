@@ -160,6 +160,14 @@ def test_full_size_properties(gpu, golden):
                             p0[idx].cpu().numpy())
     d = np.abs(a[idx].detach().cpu().numpy() - ref)
     assert d.max() <= 1e-3 and d.mean() <= 1e-6
+    # the bench's own precision: bf16 MFMA operands at B = 256
+    a16, info16 = attack_utils.emb_attack(m, vc, at, 0.1, 50, ptb0=p0, precision="bf16", return_info=True)
+    b16 = attack_utils.emb_attack(m, vc, at, 0.1, 50, ptb0=p0, precision="bf16")
+    assert torch.equal(a16, b16)
+    assert float((a16 - vc).abs().max()) <= 0.1 + 1e-6
+    L16 = info16["losses"].cpu().numpy()
+    assert np.all(L16[-1] < L16[0])
+    assert float((a16 - a).abs().max()) <= 2e-2          # SURVEY 8(c) bf16 adv bound (n <= 100)
 
 
 def test_bf16_mode_tracks_fp32(gpu, golden):
@@ -201,4 +209,11 @@ def test_multi_gpu_driver_matches_single(gpu, golden):
     vc, at, p0 = (torch.randn(5, 80, 32, generator=g).to(gpu) for _ in range(3))
     one = attack_utils.emb_attack(m, vc, at, 0.1, 8, ptb0=p0).detach()
     two = shard.emb_attack_multi_gpu([m, m], vc, at, 0.1, 8, ptb0=p0).detach()
+    assert torch.equal(one, two)
+    # configs[3]'s attack (fb) through the same driver on the full config
+    zf = golden("full_T128")
+    mf = model_from_fixture(zf).to(gpu)
+    src, vc, at, p0 = (torch.randn(5, 80, 64, generator=g).to(gpu) for _ in range(4))
+    one = attack_utils.fb_attack(mf, src, vc, at, 0.1, 4, ptb0=p0).detach()
+    two = shard.attack_multi_gpu("fb", [mf, mf], src, vc, at, 0.1, 4, ptb0=p0).detach()
     assert torch.equal(one, two)

@@ -67,6 +67,31 @@ def test_vc_attack_bf16_tracks_fp32(full, kind):
 
 
 @pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_vc_bf16_objective_after_1500(full, kind):
+    """SURVEY.md 8(c) bf16 bound at the bench horizon (n_iters = 1500) for e2e / fb: the final
+    objective term the attack drives down -- MSE(inference(src, adv), inference(src, adv_tgt))
+    (e2e, attack_utils.py:41) or MSE(SE(inference(src, adv)), SE(adv_tgt)) (fb, 123-124) -- of
+    the bf16 attack is within 5 % (relative) of the fp32 attack's, per utterance, and both
+    attacks made progress."""
+    z, m = full
+    g = torch.Generator().manual_seed(21 if kind == "e2e" else 22)
+    src, vc, at, p0 = (torch.randn(4, 80, 128, generator=g).to(DEV) for _ in range(4))
+    fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
+    a32 = fn(m, src, vc, at, 0.1, 1500, ptb0=p0).detach()
+    a16 = fn(m, src, vc, at, 0.1, 1500, ptb0=p0, precision="bf16").detach()
+
+    def objective(x):
+        out = m.inference(src, x)
+        if kind == "e2e":
+            return ((out - m.inference(src, at)) ** 2).mean((1, 2))
+        se = m.speaker_encoder
+        return ((se(out) - se(at)) ** 2).mean(1)
+    l0, l32, l16 = objective(vc), objective(a32), objective(a16)
+    assert (l32 < l0).all() and (l16 < l0).all(), (l0, l32, l16)
+    assert float(((l16 - l32).abs() / l32).max()) <= 0.05, (l16, l32)
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
 def test_vc_attack_deterministic_and_shard_invariant(full, kind):
     z, m = full
     g = torch.Generator().manual_seed(9)
