@@ -19,7 +19,7 @@ MAX_BLOCKS = 16
 
 PREC = {"fp32": 0, "bf16": 1}
 REDUCE = {"independent": 0, "mean": 1}
-ENGINE = {"auto": 0, "layered": 1, "fused": 2}
+ENGINE = {"auto": 0, "layered": 1, "fused": 2, "long": 3}
 
 
 class SECfg(ctypes.Structure):
@@ -323,7 +323,7 @@ class Context:
         return out, losses, grad0
 
     def set_engine(self, engine: str = "auto"):
-        """"auto" | "layered" | "fused" (include/avc.h AVC_ENGINE_*)."""
+        """"auto" | "layered" | "fused" | "long" (include/avc.h AVC_ENGINE_*)."""
         _check(lib().avc_set_engine(self.h, ENGINE[engine]))
 
     def engine_for(self, T: int) -> str:

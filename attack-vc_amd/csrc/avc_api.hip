@@ -31,6 +31,10 @@ template <int PREC, int SH>
 __global__ void se_fwd_fused(FusedArgs A);
 template <int PREC, int SH>
 __global__ void se_bwd_fused(FusedArgs A);
+template <int PREC>
+__global__ void lz_se_fwd(FusedArgs A, LongArgs L);
+template <int PREC>
+__global__ void lz_se_bwd(FusedArgs A, LongArgs L);
 template <int PREC, int SH>
 __global__ void dec_fwd_fused(DecArgs A);
 template <int PREC, int SH>
@@ -79,7 +83,8 @@ struct HostConv {
     const float* b;
 };
 
-enum LaunchKind { L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD, L_DZ_FWD, L_DZ_BWD, L_DENSE };
+enum LaunchKind { L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD, L_DZ_FWD, L_DZ_BWD, L_DENSE, L_LZ_FWD, L_LZ_BWD };
+constexpr size_t LZ_SHMEM = 160 * 1024;   // the long kernels use the whole LDS (avc_long.hip)
 
 // conv_gemm instantiations (avc_gemm_variants.h); the planner autotunes one per
 // launch and precision on first use of a workspace.
@@ -110,7 +115,8 @@ struct Launch {
     Problem* dprobs = nullptr;   // device problem table (L_GEMM*)
     int nprob = 0;
     HeadArgs head{};
-    FusedArgs fz{};              // L_FZ_*: per-utterance fused SpeakerEncoder pass (prec = PREC_*)
+    FusedArgs fz{};              // L_FZ_* / L_LZ_*: per-utterance SpeakerEncoder pass (prec = PREC_*)
+    LongArgs lz{};               // L_LZ_*: the long engine's scratch
     int fz_shape = 8;            // L_FZ_*: kernel shape SH (0 = standard config at T = 128, else 1|2|4|8)
     DecArgs dz{};                // L_DZ_*: per-utterance fused Decoder pass (shape: fz_shape 0 | 8)
     DenseArgs dn{};              // L_DENSE: batched conv_affine layer (or its transpose)
@@ -133,7 +139,9 @@ struct Workspace {
     DevBuf loss_cur;                  // fused head: [B] per-utterance loss of the current iteration
     unsigned long long* masks = nullptr;   // fused path: ReLU' ballot words [B][mask_words]
     int mask_words = 0;
-    bool fused = false;               // this (B, T) runs on the fused engine
+    bool fused = false;               // this (B, T) runs on the fused family (fused or long engine)
+    bool lz = false;                  // ... on the long engine (T > 128, or forced)
+    LongArgs lza{};                   // long engine: scratch (images, fp32 streams, ballot masks)
     int iters_cap = 0;
     int* step = nullptr;
     Plan fwd, iter, iter_bf16;
@@ -421,6 +429,9 @@ static int set_fused_attrs() {
                                                AVC_FZ_FNS(8)};
 #undef AVC_FZ_FNS
     for (auto& fn : fns) HIPCHK(hipFuncSetAttribute(fn.first, hipFuncAttributeMaxDynamicSharedMemorySize, fn.second));
+    for (const void* fn : {(const void*)lz_se_fwd<PREC_F32>, (const void*)lz_se_fwd<PREC_BF16>,
+                           (const void*)lz_se_bwd<PREC_F32>, (const void*)lz_se_bwd<PREC_BF16>})
+        HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LZ_SHMEM));
     return 0;
 }
 
@@ -684,7 +695,12 @@ static void free_ws(Workspace& ws) {
     ws.step = nullptr;
     if (ws.masks) hipFree(ws.masks);
     ws.masks = nullptr;
+    if (ws.lza.img[0]) hipFree(ws.lza.img[0]);
+    if (ws.lza.fl[0]) hipFree(ws.lza.fl[0]);
+    if (ws.lza.masks) hipFree(ws.lza.masks);
+    ws.lza = LongArgs{};
     ws.fused = false;
+    ws.lz = false;
     ws.built = false;
     ws.B = ws.T = 0;
     ws.iters_cap = 0;
@@ -1102,18 +1118,20 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
     const avc_se_cfg& c = ctx->cfg;
     const int B = ws.B;
     Launch F;
-    F.kind = L_FZ_FWD;
+    F.kind = ws.lz ? L_LZ_FWD : L_FZ_FWD;
     F.prec = prec;
     F.grid = dim3(B);
     F.block = dim3(256);
-    F.shmem = fz_lds_fwd(prec, ws.T, c.kernel_size);
+    F.shmem = ws.lz ? LZ_SHMEM : fz_lds_fwd(prec, ws.T, c.kernel_size);
     F.fz = fused_args(ctx, ws, prec);
+    F.lz = ws.lza;
     F.fz.x = x;
     F.fz.write_masks = attack ? 1 : 0;
     F.fz.tick = attack ? ws.step : nullptr;
     F.fz_shape = fused_shape(ctx, ws.T);
     F.flop = fz_fwd_flop(c, ws.Tl, ctx->bank_k) * B;
     F.name = prec == PREC_F32 ? "se_fwd_fused<f32>" : "se_fwd_fused<bf16>";
+    if (ws.lz) F.name = prec == PREC_F32 ? "lz_se_fwd<f32>" : "lz_se_fwd<bf16>";
 
     Launch L;
     L.kind = L_HEAD_V;
@@ -1155,7 +1173,7 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
     // fewer per iteration; AVC_FUSE_HEAD=0 keeps the separate se_head_v launch (A/B runs)
     const char* fe = getenv("AVC_FUSE_HEAD");
     // (standard shape only: the in-kernel chain is unrolled for its n_dense = 6)
-    if (attack && prec == PREC_BF16 && ctx->head_Wr16.p && c.c_h == FZ_C && c.c_out == FZ_C && F.fz_shape == 0 &&
+    if (attack && prec == PREC_BF16 && ctx->head_Wr16.p && c.c_h == FZ_C && c.c_out == FZ_C && !ws.lz && F.fz_shape == 0 &&
         c.n_dense_blocks == 6 && !(fe && fe[0] == '0')) {
         const size_t head_lds = (size_t)(4 * c.n_dense_blocks + 8) * FZ_C * sizeof(float);
         F.shmem = std::max(F.shmem, head_lds);
@@ -1174,12 +1192,13 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
 
 static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) {
     Launch L;
-    L.kind = L_FZ_BWD;
+    L.kind = ws.lz ? L_LZ_BWD : L_FZ_BWD;
     L.prec = prec;
     L.grid = dim3(ws.B);
     L.block = dim3(256);
-    L.shmem = fz_lds_bwd(prec, ws.T);
+    L.shmem = ws.lz ? LZ_SHMEM : fz_lds_bwd(prec, ws.T);
     L.fz = fused_args(ctx, ws, prec);
+    L.lz = ws.lza;
     L.fz_shape = fused_shape(ctx, ws.T);
     AdamArgs& A = L.fz.adam;
     A.ptb = ws.ptb.p;
@@ -1195,6 +1214,7 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
     A.adam_eps = 1e-8f;
     L.flop = fz_fwd_flop(ctx->cfg, ws.Tl, ctx->bank_k) * ws.B;   // input-gradient only
     L.name = prec == PREC_F32 ? "se_bwd_fused<f32>" : "se_bwd_fused<bf16>";
+    if (ws.lz) L.name = prec == PREC_F32 ? "lz_se_bwd<f32>" : "lz_se_bwd<bf16>";
     pl.launches.push_back(L);
     return 0;
 }
@@ -1219,13 +1239,43 @@ static int plan_iteration(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) {
 
 static int autotune(avc_ctx* ctx, Plan& pl);
 
-// fused per-utterance engine for this T?  (AVC_FUSED=0 in the environment forces the
-// layered engine for A/B runs)
-static bool want_fused(avc_ctx* ctx, int T) {
-    if (ctx->engine == AVC_ENGINE_LAYERED) return false;
+// Engine of a call with T frames: the fused engine up to 128 frames, the long engine above
+// (same kernels family, activations chunked through global scratch), the layered engine for
+// configs neither is built for.  AVC_FUSED=0 (AUTO only) forces layered, AVC_LONG=1 long.
+static int engine_for(avc_ctx* ctx, int T) {
+    if (ctx->engine == AVC_ENGINE_LAYERED || !ctx->fused_ok) return AVC_ENGINE_LAYERED;
     const char* fe = getenv("AVC_FUSED");
-    if (ctx->engine == AVC_ENGINE_AUTO && fe && fe[0] == '0') return false;
-    return ctx->fused_ok && T <= 128;
+    if (ctx->engine == AVC_ENGINE_AUTO && fe && fe[0] == '0') return AVC_ENGINE_LAYERED;
+    const char* le = getenv("AVC_LONG");
+    if (ctx->engine == AVC_ENGINE_LONG || (le && le[0] == '1')) return AVC_ENGINE_LONG;
+    return T <= 128 ? AVC_ENGINE_FUSED : AVC_ENGINE_LONG;
+}
+static bool want_fused(avc_ctx* ctx, int T) { return engine_for(ctx, T) != AVC_ENGINE_LAYERED; }
+
+// long-engine scratch for B utterances of up to T frames and `nlayers` masked layers
+static int alloc_long(LongArgs& L, int B, int T, int nlayers) {
+    const int rows = T + 2 * LZ_ZR + 64;
+    L.img_stride = (int64_t)rows * 128 * 4;                 // fp32-sized rows serve both precisions
+    L.fl_stride = (int64_t)((T + 32 + 15) / 16 + LZ_FL_EXTRA) * 4 * 2 * 64 * 4;
+    L.nFmax = (T + 15) / 16;
+    L.mask_stride = (int64_t)nlayers * L.nFmax * 32;
+    char* img = nullptr;
+    float* fl = nullptr;
+    unsigned long long* mk = nullptr;
+    HIPCHK(hipMalloc(&img, 3 * (size_t)B * L.img_stride));
+    HIPCHK(hipMalloc(&fl, 3 * (size_t)B * L.fl_stride * sizeof(float)));
+    HIPCHK(hipMalloc(&mk, (size_t)B * L.mask_stride * sizeof(unsigned long long)));
+    // every byte a kernel may stage is finite from the start (weights past K are zero, and
+    // 0 * NaN would not be)
+    HIPCHK(hipMemset(img, 0, 3 * (size_t)B * L.img_stride));
+    HIPCHK(hipMemset(fl, 0, 3 * (size_t)B * L.fl_stride * sizeof(float)));
+    HIPCHK(hipMemset(mk, 0, (size_t)B * L.mask_stride * sizeof(unsigned long long)));
+    for (int i = 0; i < 3; ++i) {
+        L.img[i] = img + (size_t)i * B * L.img_stride;
+        L.fl[i] = fl + (size_t)i * B * L.fl_stride;
+    }
+    L.masks = mk;
+    return 0;
 }
 
 static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
@@ -1253,7 +1303,9 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         if (To != Tp) return fail("conv/pool length mismatch at block %d (%d vs %d)", l, To, Tp);
         Tl.push_back(To);
     }
-    const bool same = ws.built && ws.B == B && ws.T == T && ws.fused == want_fused(ctx, T);
+    const int eng = engine_for(ctx, T);
+    const bool same = ws.built && ws.B == B && ws.T == T && ws.fused == (eng != AVC_ENGINE_LAYERED) &&
+                      ws.lz == (eng == AVC_ENGINE_LONG);
     if (same && n_iters <= ws.iters_cap) return 0;
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (!same) {
@@ -1263,7 +1315,8 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         ws.Tl = Tl;
         const int nb = ctx->nb;
         const size_t X = (size_t)B * c.c_in * T;
-        ws.fused = want_fused(ctx, T);
+        ws.fused = eng != AVC_ENGINE_LAYERED;
+        ws.lz = eng == AVC_ENGINE_LONG;
         int rc = 0;
         for (DevBuf* b : {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.grad0}) rc |= dalloc(*b, X);
         for (DevBuf* b : {&ws.emb_fwd, &ws.org, &ws.tgt}) rc |= dalloc(*b, (size_t)B * c.c_out);
@@ -1273,6 +1326,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
             rc |= dalloc(ws.gpooled, (size_t)B * FZ_C);
             rc |= dalloc(ws.loss_cur, (size_t)B);
             HIPCHK(hipMalloc(&ws.masks, (size_t)B * ws.mask_words * sizeof(unsigned long long)));
+            if (ws.lz && alloc_long(ws.lza, B, T, nb + 1 + 2 * c.n_conv_blocks)) return 1;
         } else {
             rc |= dalloc(ws.gxd, X);
             rc |= dalloc(ws.bank, (size_t)B * nb * c.c_bank * T);
@@ -1411,6 +1465,14 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
     }
     case L_DENSE:
         klaunch(ev, false, dense_batched, L.grid, L.block, 0, s, L.dn);
+        return hipGetLastError();
+    case L_LZ_FWD:
+        if (L.prec == PREC_F32) klaunch(ev, false, lz_se_fwd<PREC_F32>, L.grid, L.block, L.shmem, s, L.fz, L.lz);
+        else klaunch(ev, false, lz_se_fwd<PREC_BF16>, L.grid, L.block, L.shmem, s, L.fz, L.lz);
+        return hipGetLastError();
+    case L_LZ_BWD:
+        if (L.prec == PREC_F32) klaunch(ev, false, lz_se_bwd<PREC_F32>, L.grid, L.block, L.shmem, s, L.fz, L.lz);
+        else klaunch(ev, false, lz_se_bwd<PREC_BF16>, L.grid, L.block, L.shmem, s, L.fz, L.lz);
         return hipGetLastError();
     default:
         return hipErrorInvalidValue;
@@ -1584,9 +1646,10 @@ extern "C" int avc_se_forward(avc_ctx* ctx, const float* x, int B, int T, float*
 
 extern "C" int avc_set_engine(avc_ctx* ctx, int engine) {
     if (!ctx) return fail("null ctx");
-    if (engine != AVC_ENGINE_AUTO && engine != AVC_ENGINE_LAYERED && engine != AVC_ENGINE_FUSED)
+    if (engine != AVC_ENGINE_AUTO && engine != AVC_ENGINE_LAYERED && engine != AVC_ENGINE_FUSED &&
+        engine != AVC_ENGINE_LONG)
         return fail("bad engine %d", engine);
-    if (engine == AVC_ENGINE_FUSED && !ctx->fused_ok)
+    if ((engine == AVC_ENGINE_FUSED || engine == AVC_ENGINE_LONG) && !ctx->fused_ok)
         return fail("the fused engine needs c_in=80, c_h=c_bank=c_out=128, bank_scale=1, bank_size<=8, odd kernel_size<=5, "
                     "<=8 conv blocks with subsample 1 or 2");
     ctx->engine = engine;
@@ -1595,7 +1658,7 @@ extern "C" int avc_set_engine(avc_ctx* ctx, int engine) {
 
 extern "C" int avc_get_engine(avc_ctx* ctx, int T) {
     if (!ctx) return -1;
-    return want_fused(ctx, T) ? AVC_ENGINE_FUSED : AVC_ENGINE_LAYERED;
+    return engine_for(ctx, T);
 }
 
 extern "C" int avc_set_profiling(avc_ctx* ctx, int enable) {

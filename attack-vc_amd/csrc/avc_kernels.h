@@ -173,6 +173,34 @@ struct FusedArgs {
 };
 
 // ---------------------------------------------------------------------------------
+// Long-utterance engine (avc_long.hip): any T (the fused engine's LDS images stop at 128
+// frames).  Still one workgroup of 4 waves per utterance and wave w owns channels
+// [32w, 32w+32), but the activations live in per-utterance global scratch (L2 / MALL):
+//   operand images  [LZ_ZR pad rows | frames | pad rows][128 channels] of the operand type
+//                   (bf16 / fp32), reflect-mirror or zero pad rows written by the producer;
+//   fp32 streams    the residual h, its gradient and raw GEMM outputs, in the MFMA C/D
+//                   "fragment layout" [16-frame fragment][wave][tile][64 lanes] f32x4, so an
+//                   epilogue reads / writes one coalesced 1 KiB run per wave instruction;
+//   ReLU' masks     64-bit ballots per (layer, 16-frame fragment, wave, tile, row), so any
+//                   16-aligned frame chunking reads them back.
+// Each layer runs over chunks of 128 output frames: the chunk's input rows are staged into
+// LDS and the layer's GEMM runs on MFMA exactly as in the fused engine.
+// ---------------------------------------------------------------------------------
+constexpr int LZ_ZR = 16;         // pad rows before frame 0 / after the last frame of an image
+constexpr int LZ_FL_EXTRA = 4;    // fragments beyond ceil(T/16) in a fragment-layout stream
+
+struct LongArgs {
+    char* img[3];                     // operand images, per utterance img_stride bytes each
+    int64_t img_stride;
+    float* fl[3];                     // fp32 fragment-layout streams, fl_stride floats per utterance
+    int64_t fl_stride;
+    unsigned long long* masks;        // ballot words [B][layer][nFmax][wave][tile*4 + row]
+    int64_t mask_stride;              // words per utterance
+    int32_t nFmax;                    // fragments per layer in the mask layout
+    int32_t pad_;
+};
+
+// ---------------------------------------------------------------------------------
 // Fused per-utterance Decoder (avc_vc.hip, models.py:346-435) for the e2e / feedback
 // attacks.  Same layout rules as the SpeakerEncoder engine: wave w owns channels
 // [32w, 32w+32) of every 128-channel layer.  A x2 pixel-shuffle conv (128 -> 256

@@ -1,0 +1,907 @@
+// Long-utterance engine: the SpeakerEncoder / ContentEncoder forward, the SpeakerEncoder
+// input-gradient + Adam, for ANY number of frames T (real utterances are 128-600 frames;
+// the fused engine's LDS-resident images stop at T = 128).
+//
+// Same mapping as the fused engine (avc_fused.hip): one workgroup of 4 waves owns one
+// utterance; wave w owns output channels [32w, 32w+32) of every 128-channel layer; every
+// Conv1d and Conv1d input-gradient is a GEMM C[out ch][frames] = A[out ch][(tap, in ch)] x
+// B on v_mfma_f32_16x16x32_bf16 (bf16) / v_mfma_f32_16x16x4_f32 (fp32), with A streamed
+// from L2 through the cross-GEMM register ring (avc_fused_core.h).  What changes:
+//
+//  * activations live in per-utterance global scratch (LongArgs, avc_kernels.h): operand
+//    images [pad rows | frames | pad rows][128 ch] (reflect-mirror rows for a forward
+//    conv, zero rows for an input-gradient), and fp32 streams (the residual h, its
+//    gradient) in the MFMA C/D fragment layout, so an epilogue moves one coalesced 1 KiB
+//    run per wave instruction;
+//  * every layer runs over chunks of 128 output columns: the chunk's input rows (+ the
+//    conv halo) are staged into an LDS image with the fused engine's conflict-free row
+//    stride, then the fused engine's K loop runs unchanged.  The last chunk of a layer is
+//    moved back to end at the layer's last fragment (it overlaps its predecessor; columns
+//    are recomputed bitwise identically and only the owning chunk accumulates sums);
+//  * an input-gradient's columns are the reflect-PADDED input positions v = n - OFF, so
+//    the pad positions' sums sit in the same chunk as the interior frames they fold onto
+//    (models.py:23-29 adjoint, lz_fold), for any T;
+//  * ReLU' masks are 64-bit ballots per 16-frame fragment (chunking-independent).
+//
+// Per-layer frame counts are runtime values, but every GEMM runs a compile-time number of
+// fragments (8 per chunk; columns past the layer are clamped reads and dropped writes).
+#include "avc_fused_core.h"
+
+namespace avc {
+
+constexpr int LZ_CHF = 8;           // fragments per chunk (128 columns)
+
+template <int PREC>
+struct Lz {
+    using E = typename Fz<PREC>::E;
+    static constexpr int ESZ = (int)sizeof(E);
+    static constexpr int RS = Fz<PREC>::RS;     // LDS row stride
+    static constexpr int GRB = 128 * ESZ;       // global image row bytes
+};
+
+__device__ __forceinline__ int lz_nf(int frames) { return (frames + 15) >> 4; }
+
+// Chunk k of a layer of nfrag fragments: starts at fragment chf*k, except the last, which
+// is moved back to end at nfrag.  A chunk owns the columns [16 f0, own_hi) up to the next
+// chunk's start (the last one owns to the end), so every column is owned exactly once and
+// a reflect-pad fold (whose sources and targets share the last / first chunk) is always
+// complete in the chunk that owns its targets.  Returns false past the last chunk.
+struct LzChunk {
+    int f0, own_hi;
+    bool last;
+    __device__ __forceinline__ bool owns(int col) const { return col >= 16 * f0 && col < own_hi; }
+};
+__device__ __forceinline__ bool lz_chunk(int k, int nfrag, int chf, LzChunk& ch) {
+    const int f = k * chf;
+    if (k > 0 && f >= nfrag) return false;
+    // the moved-back last chunk never starts before fragment 2: the first chunk keeps the
+    // left reflect pads' targets (frames <= 4, columns <= 20) together with their sources
+    const int flast = nfrag > chf ? max(nfrag - chf, 2) : 0;
+    ch.last = f + chf >= nfrag;
+    ch.f0 = ch.last ? flast : f;
+    const int fn = f + chf;
+    ch.own_hi = ch.last ? 1 << 30 : 16 * (fn + chf >= nfrag ? flast : fn);
+    return true;
+}
+
+// rows [r0, r0 + n) of a global operand image -> LDS rows [0, n) (stride RS); whole
+// workgroup, 16-byte pieces, U pieces per thread in flight
+template <int PREC>
+__device__ __forceinline__ void lz_stage(char* lds, const char* img, int r0, int n) {
+    constexpr int GRB = Lz<PREC>::GRB, RS = Lz<PREC>::RS;
+    constexpr int PPR = GRB / 16;
+    constexpr int U = 8;
+    const int tot = n * PPR;
+    const char* src = img + (size_t)r0 * GRB;
+    for (int base = 0; base < tot; base += 256 * U) {
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int idx = min(base + threadIdx.x + 256 * u, tot - 1);
+            v[u] = *reinterpret_cast<const f32x4*>(src + (size_t)idx * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int idx = base + threadIdx.x + 256 * u;
+            if (idx < tot) {
+                const int r = idx / PPR, p = idx - r * PPR;
+                *reinterpret_cast<f32x4*>(lds + r * RS + p * 16) = v[u];
+            }
+        }
+    }
+}
+
+// zero image rows [r0, r0 + n) (whole workgroup)
+template <int PREC>
+__device__ __forceinline__ void lz_zero_rows(char* img, int r0, int n) {
+    constexpr int GRB = Lz<PREC>::GRB;
+    const int tot = n * GRB / 16;
+    f32x4* p = reinterpret_cast<f32x4*>(img + (size_t)r0 * GRB);
+    for (int i = threadIdx.x; i < tot; i += 256) p[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// global stores of this workgroup visible to its other waves
+__device__ __forceinline__ void lz_publish() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// this lane's f32x4 of frame t (channels 32w + 16i + 4kq .. +3) in a fragment-layout stream
+__device__ __forceinline__ f32x4* lz_fl(float* buf, int t, int w, int i) {
+    const int kq = (threadIdx.x & 63) >> 4;
+    return reinterpret_cast<f32x4*>(buf) + ((((t >> 4) * 4 + w) * 2 + i) * 64 + ((t & 15) | (kq << 4)));
+}
+
+// frame t of an operand image, 4 consecutive channels at byte offset chb; mirror rows of
+// the reflect pad (F.pad mode="reflect", models.py:23-29) for pads up to 4
+template <int PREC>
+__device__ __forceinline__ void lz_put(char* img, int t, int T, int chb, f32x4 v) {
+    constexpr int GRB = Lz<PREC>::GRB;
+    st4<PREC>(img + (size_t)(LZ_ZR + t) * GRB + chb, v);
+    if (t >= 1 && t <= 4) st4<PREC>(img + (size_t)(LZ_ZR - t) * GRB + chb, v);
+    if (t >= T - 5 && t <= T - 2) st4<PREC>(img + (size_t)(LZ_ZR + 2 * T - 2 - t) * GRB + chb, v);
+}
+
+// ReLU' ballots of one fragment: word (i, r) bit (16 kq + c) = (y[i][r] > 0)
+__device__ __forceinline__ void lz_mask_store(u64* words, const f32x4 (&y)[2]) {
+    u64 b[8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[4 * i + r] = __ballot(y[i][r] > 0.f);
+    if ((threadIdx.x & 63) == 0) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) reinterpret_cast<u64x2*>(words)[k] = u64x2{b[2 * k], b[2 * k + 1]};
+    }
+}
+struct LzMask {
+    u64 b[8];
+    __device__ __forceinline__ void load(const u64* words) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] = words[k];
+    }
+    __device__ __forceinline__ void none() {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] = 0;
+    }
+    __device__ __forceinline__ float act(int i, int r, int actk) const {
+        return ((b[4 * i + r] >> (threadIdx.x & 63)) & 1ull) ? 1.f : (actk ? 0.01f : 0.f);
+    }
+};
+
+// Reflect-pad adjoint inside a chunk of an input-gradient over padded positions
+// v = n - OFF (column n = 16 (f0 + f) + c): the sum at pad position v in [-E, 0) folds onto
+// frame -v, at v in [Tin, Tin + E) onto 2 (Tin - 1) - v.  Pads and targets of one side
+// always share a chunk (the domain starts OFF >= E columns early and the last chunk is
+// moved back).  Per-wave scratch [MT*16 rows][2E]; contains a barrier (all waves call it).
+template <int MT, int NFL = LZ_CHF>
+__device__ __forceinline__ void lz_fold(f32x4 (&acc)[MT][LZ_CHF], int f0, int OFF, int Tin, int E, float* scr) {
+    const int lane = threadIdx.x & 63, c = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int f = 0; f < NFL; ++f) {
+        const int v = 16 * (f0 + f) + c - OFF;
+        const int e = v < 0 ? v + E : v - Tin + E;
+        if ((v < 0 && v >= -E) || (v >= Tin && v < Tin + E)) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) scr[(16 * i + 4 * kq + r) * 8 + e] = acc[i][f][r];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < NFL; ++f) {
+        const int t = 16 * (f0 + f) + c - OFF;
+        const int el = (t >= 1 && t <= E) ? E - t : -1;
+        const int er = (t >= Tin - 1 - E && t <= Tin - 2) ? E + Tin - 2 - t : -1;
+        if (el >= 0 || er >= 0) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float* row = scr + (16 * i + 4 * kq + r) * 8;
+                    float add = el >= 0 ? row[el] : 0.f;
+                    if (er >= 0) add += row[er];
+                    acc[i][f][r] += add;
+                }
+        }
+    }
+    __syncthreads();
+}
+
+// InstanceNorm statistics (affine=False, eps 1e-5, biased variance; models.py:176) of the
+// rows this wave owns over the Tl frames of a fragment-layout raw stream: s = sum of the
+// rows (accumulated by the GEMM epilogues over owned columns), then the centred second
+// moment in a second pass.  mean / invstd per (tile, row).
+__device__ __forceinline__ void lz_in_stats(const float* raw, int Tl, int w, f32x4 (&s)[2], f32x4 (&mean)[2],
+                                            f32x4 (&invstd)[2]) {
+    const int c = threadIdx.x & 15;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        row16_sum(s[i]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mean[i][r] = s[i][r] / (float)Tl;
+    }
+    f32x4 q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int nf = lz_nf(Tl);
+    for (int F = 0; F < nf; ++F) {
+        const int t = 16 * F + c;
+        if (t < Tl)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const f32x4 d = *lz_fl(const_cast<float*>(raw), t, w, i) - mean[i];
+                q[i] += d * d;
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        row16_sum(q[i]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) invstd[i][r] = 1.f / sqrtf(q[i][r] / (float)Tl + 1e-5f);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// forward: SpeakerEncoder (models.py:327-343) or, in ce_mode, ContentEncoder (181-210)
+// ---------------------------------------------------------------------------------
+template <int PREC>
+__global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
+    using Z = Lz<PREC>;
+    constexpr int RS = Z::RS, ESZ = Z::ESZ, GRB = Z::GRB;
+    constexpr int VE = 16 / ESZ, KS = 4 * VE;
+    constexpr int NF = LZ_CHF;
+    constexpr bool DBUF = PREC == PREC_BF16;
+    const int b = blockIdx.x;
+    const int T = A.T, nb = A.nb, nblk = A.nblk, ks = A.ks, P = ks / 2, act = A.act;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, kq = lane >> 4;
+    const int ch0 = 32 * w + 4 * kq;
+    const bool ce = A.ce_mode != 0;
+    const bool wm = A.write_masks != 0 && !ce;
+    if (A.tick && b == 0 && tid == 0) atomicAdd(A.tick, 1);
+
+    char* imgx = L.img[0] + (size_t)b * L.img_stride;
+    char* imgh = L.img[1] + (size_t)b * L.img_stride;
+    char* imgy = L.img[2] + (size_t)b * L.img_stride;
+    float* hf[2] = {L.fl[0] + (size_t)b * L.fl_stride, L.fl[1] + (size_t)b * L.fl_stride};
+    float* raw = L.fl[2] + (size_t)b * L.fl_stride;
+    u64* mk = L.masks + (size_t)b * L.mask_stride;
+    auto mword = [&](int layer, int F) __attribute__((always_inline)) {
+        return mk + ((size_t)(layer * L.nFmax + F) * 4 + w) * 8;
+    };
+
+    const int ns_c = ks * FZ_C / KS;
+    auto op_bank = [&](int kb) __attribute__((always_inline)) {
+        const int ns = (FZ_CIN * (kb + 1) + KS - 1) / KS;
+        return aop(A.w.bank[kb], 2 * w, 2, ns, ns);
+    };
+    auto op_inb = [&](int kb) __attribute__((always_inline)) { return aop(A.w.in_b[kb], 2 * w, 2, FZ_C / KS, FZ_C / KS); };
+    auto op_inx = [&]() __attribute__((always_inline)) {
+        const int ns = (FZ_CIN + KS - 1) / KS;
+        return aop(A.w.in_x, 2 * w, 2, ns, ns);
+    };
+    auto op_c1 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_mean = [&]() __attribute__((always_inline)) { return aop(A.w.mean_w, 2 * w, 2, FZ_C / KS, FZ_C / KS); };
+    ARing<2> ring;
+    ring_fill(ring, op_bank(0));
+
+    // ---- x [80][T] -> image rows (transposed; reflect mirrors for the bank's pads <= 4)
+    {
+        constexpr int NGX = FZ_CIN / VE;
+        const float* xs = A.x + (size_t)b * FZ_CIN * T;
+        for (int idx = tid; idx < NGX * T; idx += 256) {
+            const int g = idx / T, t = idx - g * T;
+            f32x4 v;
+            if constexpr (PREC == PREC_F32) {
+                v = f32x4{xs[(size_t)(4 * g) * T + t], xs[(size_t)(4 * g + 1) * T + t], xs[(size_t)(4 * g + 2) * T + t],
+                          xs[(size_t)(4 * g + 3) * T + t]};
+            } else {
+                bf16x8 h;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) h[e] = (__bf16)xs[(size_t)(8 * g + e) * T + t];
+                v = __builtin_bit_cast(f32x4, h);
+            }
+            *reinterpret_cast<f32x4*>(imgx + (size_t)(LZ_ZR + t) * GRB + 16 * g) = v;
+            if (t >= 1 && t <= 4) *reinterpret_cast<f32x4*>(imgx + (size_t)(LZ_ZR - t) * GRB + 16 * g) = v;
+            if (t >= T - 5 && t <= T - 2)
+                *reinterpret_cast<f32x4*>(imgx + (size_t)(LZ_ZR + 2 * T - 2 - t) * GRB + 16 * g) = v;
+        }
+    }
+    lz_publish();
+
+    int rb[NF];
+    f32x4 in_s[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // ContentEncoder: IN row sums
+    // ---- conv bank (models.py:82-104) + in_conv (337-338), chunk by chunk: the bank
+    // outputs of a chunk never leave LDS (in_conv consumes them block by block)
+    {
+        constexpr int NXR = 128 + 10;                   // x window: frames n0-4 .. n0+131 (+1)
+        char* XB = fz_lds;
+        char* BK0 = XB + NXR * RS;
+        char* BK1 = DBUF ? BK0 + 128 * RS : BK0;
+        const int nf0 = lz_nf(T);
+        f32x4 b_in[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) b_in[i] = *reinterpret_cast<const f32x4*>(A.w.b_in + ch0 + 16 * i);
+        LzChunk chk;
+        for (int k = 0; lz_chunk(k, nf0, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            __syncthreads();                             // the previous chunk's readers are done
+            lz_stage<PREC>(XB, imgx, LZ_ZR + n0 - 4, NXR);
+            __syncthreads();
+            f32x4 acc_h[2][NF];
+            zero_acc(acc_h);
+            for (int kb = 0; kb < nb; ++kb) {
+                const int kk = kb + 1, pl = kk / 2;
+                f32x4 bkb[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) bkb[i] = *reinterpret_cast<const f32x4*>(A.w.b_bank[kb] + ch0 + 16 * i);
+                f32x4 acc[2][NF];
+                zero_acc(acc);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T - 1) - n0 + 4 - pl;
+                fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc, IC<NF>{}, ring, op_bank(kb), op_inb(kb), XB, rb);
+                char* BK = (kb & 1) ? BK1 : BK0;
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    f32x4 y[2];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) y[i][r] = act_f(acc[i][f][r] + bkb[i][r], act);
+                    if (wm && chk.f0 + f < nf0 && chk.owns(16 * (chk.f0 + f))) lz_mask_store(mword(kb, chk.f0 + f), y);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) st4<PREC>(BK + (16 * f + c) * RS + (ch0 + 16 * i) * ESZ, y[i]);
+                }
+                __syncthreads();
+#pragma unroll
+                for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T - 1) - n0;
+                const AOp nxt = kb + 1 < nb ? op_bank(kb + 1) : op_inx();
+                fz_gemm<PREC, 2, NF, FZ_C, 1>(acc_h, IC<NF>{}, ring, op_inb(kb), nxt, BK, rb);
+                if (!DBUF) __syncthreads();
+            }
+#pragma unroll
+            for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T - 1) - n0 + 4;
+            fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc_h, IC<NF>{}, ring, op_inx(), chk.last ? op_c1(0) : op_bank(0), XB, rb);
+            // h0 = act(in_conv + b) (SpeakerEncoder) / raw in_conv + b (ContentEncoder: IN next)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = n0 + 16 * f + c;
+                f32x4 y[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    y[i] = acc_h[i][f] + b_in[i];
+                    if (!ce)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) y[i][r] = act_f(y[i][r], act);
+                }
+                if (wm && chk.f0 + f < nf0 && chk.owns(16 * (chk.f0 + f))) lz_mask_store(mword(nb, chk.f0 + f), y);
+                if (t < T)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (ce) {
+                            *lz_fl(raw, t, w, i) = y[i];
+                            if (chk.owns(t)) in_s[i] += y[i];
+                        } else {
+                            *lz_fl(hf[0], t, w, i) = y[i];
+                            lz_put<PREC>(imgh, t, T, (ch0 + 16 * i) * ESZ, y[i]);
+                        }
+                    }
+            }
+        }
+    }
+    // ContentEncoder: h0 = act(IN(in_conv + b)) (models.py:195-200)
+    auto in_apply = [&](int Tl, auto&& out) __attribute__((always_inline)) {
+        lz_publish();
+        f32x4 mean[2], inv[2];
+        lz_in_stats(raw, Tl, w, in_s, mean, inv);
+        for (int F = 0; F < lz_nf(Tl); ++F) {
+            const int t = 16 * F + c;
+            if (t < Tl)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    f32x4 v = (*lz_fl(raw, t, w, i) - mean[i]) * inv[i];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = act_f(v[r], act);
+                    out(t, i, v);
+                }
+        }
+        in_s[0] = in_s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    if (ce)
+        in_apply(T, [&](int t, int i, f32x4 v) __attribute__((always_inline)) {
+            *lz_fl(hf[0], t, w, i) = v;
+            lz_put<PREC>(imgh, t, T, (ch0 + 16 * i) * ESZ, v);
+        });
+
+    // ---- conv blocks (models.py:285-305)
+    int cur = 0;
+    f32x4 tmean[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    char* WB = fz_lds;
+    for (int l = 0; l < nblk; ++l) {
+        const int Ti = A.Tl[l], To = A.Tl[l + 1], s = A.sub[l];
+        const bool lastblk = l + 1 == nblk;
+        f32x4 bc1[2], bc2[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            bc1[i] = *reinterpret_cast<const f32x4*>(A.w.b_c1[l] + ch0 + 16 * i);
+            bc2[i] = *reinterpret_cast<const f32x4*>(A.w.b_c2[l] + ch0 + 16 * i);
+        }
+        lz_publish();                                   // imgh of this block complete
+        // conv1 (stride 1): y1 = act(conv1(h) + b1)
+        LzChunk chk;
+        const int nfi = lz_nf(Ti);
+        for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgh, LZ_ZR + n0 - P, 127 + ks + 2);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Ti - 1) - n0;
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c1(l), chk.last ? op_c2(l) : op_c1(l), WB, rb);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = n0 + 16 * f + c;
+                f32x4 y[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    y[i] = acc[i][f] + bc1[i];
+                    if (!ce)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) y[i][r] = act_f(y[i][r], act);
+                }
+                if (wm && chk.f0 + f < nfi && chk.owns(16 * (chk.f0 + f))) lz_mask_store(mword(nb + 1 + 2 * l, chk.f0 + f), y);
+                if (t < Ti)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (ce) {
+                            *lz_fl(raw, t, w, i) = y[i];
+                            if (chk.owns(t)) in_s[i] += y[i];
+                        } else {
+                            lz_put<PREC>(imgy, t, Ti, (ch0 + 16 * i) * ESZ, y[i]);
+                        }
+                    }
+            }
+        }
+        if (ce)
+            in_apply(Ti, [&](int t, int i, f32x4 v) __attribute__((always_inline)) {
+                lz_put<PREC>(imgy, t, Ti, (ch0 + 16 * i) * ESZ, v);
+            });
+        lz_publish();                                   // imgy complete
+        // conv2 (stride s): y2 = act(conv2(y1) + b2); h = y2 + avg_pool1d(h, s, ceil_mode)
+        float* hin = hf[cur];
+        float* hout = hf[cur ^ 1];
+        const int nfo = lz_nf(To);
+        auto pool = [&](int t, int i) __attribute__((always_inline)) {
+            if (s == 1) return *lz_fl(hin, t, w, i);
+            const f32x4 a = *lz_fl(hin, 2 * t, w, i);
+            if (2 * t + 1 < Ti) return (a + *lz_fl(hin, 2 * t + 1, w, i)) / 2.f;
+            return a;
+        };
+        for (int k = 0; lz_chunk(k, nfo, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgy, LZ_ZR + s * n0 - P, s * 127 + ks + 2);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) rb[f] = s * (min(n0 + 16 * f + c, To - 1) - n0);
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            const AOp nxt = chk.last ? (!lastblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l))) : op_c2(l);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l), nxt, WB, rb);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = n0 + 16 * f + c;
+                f32x4 y[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    y[i] = acc[i][f] + bc2[i];
+                    if (!ce)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) y[i][r] = act_f(y[i][r], act);
+                }
+                if (wm && chk.f0 + f < nfo && chk.owns(16 * (chk.f0 + f))) lz_mask_store(mword(nb + 2 + 2 * l, chk.f0 + f), y);
+                if (t < To)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (ce) {
+                            *lz_fl(raw, t, w, i) = y[i];
+                            if (chk.owns(t)) in_s[i] += y[i];
+                        } else {
+                            const f32x4 h = y[i] + pool(t, i);
+                            *lz_fl(hout, t, w, i) = h;
+                            lz_put<PREC>(imgh, t, To, (ch0 + 16 * i) * ESZ, h);
+                            if (lastblk && chk.owns(t)) tmean[i] += h;
+                        }
+                    }
+            }
+        }
+        if (ce)
+            in_apply(To, [&](int t, int i, f32x4 v) __attribute__((always_inline)) {
+                const f32x4 h = v + pool(t, i);
+                *lz_fl(hout, t, w, i) = h;
+                lz_put<PREC>(imgh, t, To, (ch0 + 16 * i) * ESZ, h);
+            });
+        cur ^= 1;
+    }
+    const int TN = A.Tl[nblk];
+    if (ce) {
+        // mean_layer (1x1, models.py:207): mu = W_mean h_N + b -> [128][TN]
+        lz_publish();
+        f32x4 bm[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) bm[i] = *reinterpret_cast<const f32x4*>(A.w.b_mean + ch0 + 16 * i);
+        float* mu = A.mu_out + (size_t)b * FZ_C * TN;
+        LzChunk chk;
+        const int nfn = lz_nf(TN);
+        for (int k = 0; lz_chunk(k, nfn, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgh, LZ_ZR + n0, 129);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, TN - 1) - n0;
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_mean(), op_mean(), WB, rb);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = n0 + 16 * f + c;
+                if (t < TN)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) mu[(size_t)(ch0 + 16 * i + r) * TN + t] = acc[i][f][r] + bm[i][r];
+            }
+        }
+        return;
+    }
+    // AdaptiveAvgPool1d(1) (models.py:275,340): mean over the TN frames
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        f32x4 s4 = tmean[i];
+        row16_sum(s4);
+        if (c == 0) {
+            f32x4 m;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) m[r] = s4[r] / (float)TN;
+            *reinterpret_cast<f32x4*>(A.pooled + (size_t)b * FZ_C + ch0 + 16 * i) = m;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// backward: d loss / d pooled -> conv blocks^T -> in_conv^T -> bank^T -> tanh' + Adam
+// (attack_utils.py:78-84, torch _single_tensor_adam) or d loss / d x (gx_out)
+// ---------------------------------------------------------------------------------
+// Bank input-gradient chunk width: 128 columns in bf16; 64 in fp32 (its g_pre0 and g(b_k)
+// LDS windows at 544 B per row would not fit beside each other at 128)
+template <int PREC>
+struct LzBank {
+    static constexpr int CHF = PREC == PREC_BF16 ? 8 : 4;
+};
+
+template <int PREC>
+__global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
+    using Z = Lz<PREC>;
+    using E = typename Z::E;
+    constexpr int RS = Z::RS, ESZ = Z::ESZ, GRB = Z::GRB;
+    constexpr int VE = 16 / ESZ, KS = 4 * VE;
+    constexpr int NF = LZ_CHF;
+    const int b = blockIdx.x;
+    const int T = A.T, nb = A.nb, nblk = A.nblk, ks = A.ks, P = ks / 2, act = A.act;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, kq = lane >> 4;
+    const int ch0 = 32 * w + 4 * kq;
+
+    char* imgp = L.img[0] + (size_t)b * L.img_stride;   // g_pre0 (= g(h0) * act'(h0))
+    char* imgg = L.img[1] + (size_t)b * L.img_stride;   // dilated dY of a conv2
+    char* imgg2 = L.img[2] + (size_t)b * L.img_stride;  // dY of a conv1
+    float* gh[2] = {L.fl[0] + (size_t)b * L.fl_stride, L.fl[1] + (size_t)b * L.fl_stride};
+    const u64* mk = L.masks + (size_t)b * L.mask_stride;
+    auto mword = [&](int layer, int F) __attribute__((always_inline)) {
+        return mk + ((size_t)(layer * L.nFmax + F) * 4 + w) * 8;
+    };
+    float* FSCR = reinterpret_cast<float*>(fz_lds + 150 * 1024) + w * (5 * 16 * 8);
+
+    const int ns_c = ks * FZ_C / KS;
+    auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2T[l], 2 * w, 2, ns_c, ns_c); };
+    constexpr int SPW = 32 / KS;                        // K steps of one wave's 32-channel quarter
+    constexpr int SPT = FZ_C / KS;                      // K steps per tap
+    constexpr int LG = SPW == 1 ? 0 : 1;
+    auto op_inTb = [&](int kb) __attribute__((always_inline)) { return aop(A.w.inT_b[kb], 2 * w, 2, SPT, SPT); };
+    auto op_inTx = [&]() __attribute__((always_inline)) { return aop(A.w.inT_x, 0, 5, SPT, SPW, 30, -1, 0, w * SPW); };
+    auto op_bankT = [&](int kb) __attribute__((always_inline)) {
+        return aop(A.w.bankT[kb], 0, 5, (kb + 1) * SPT, (kb + 1) * SPW, LG, SPW - 1, SPT, w * SPW);
+    };
+    ARing<2> ring;
+    ring_fill(ring, op_c2T(nblk - 1));
+
+    // g(h_N) = d loss / d pooled / TN on every frame (AdaptiveAvgPool1d backward)
+    const int TN = A.Tl[nblk];
+    f32x4 gN[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        gN[i] = *reinterpret_cast<const f32x4*>(A.g_pooled + (size_t)b * FZ_C + ch0 + 16 * i);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gN[i][r] = gN[i][r] / (float)TN;
+    }
+    // dY of the last block's conv2 = g(h_N) * act'(y2): dilated image rows LZ_ZR + s*t
+    {
+        const int l = nblk - 1, To = A.Tl[l + 1], s = A.sub[l];
+        for (int F = 0; F < lz_nf(To); ++F) {
+            LzMask m;
+            m.load(mword(nb + 2 + 2 * l, F));
+            const int t = 16 * F + c;
+            if (t < To)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    f32x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = gN[i][r] * m.act(i, r, act);
+                    st4<PREC>(imgg + (size_t)(LZ_ZR + s * t) * GRB + (ch0 + 16 * i) * ESZ, v);
+                    if (s == 2)
+                        st4<PREC>(imgg + (size_t)(LZ_ZR + 2 * t + 1) * GRB + (ch0 + 16 * i) * ESZ,
+                                  f32x4{0.f, 0.f, 0.f, 0.f});
+                }
+        }
+    }
+    int rb[NF];
+    char* WB = fz_lds;
+    int cur = 0;
+    for (int l = nblk - 1; l >= 0; --l) {
+        const int Ti = A.Tl[l], To = A.Tl[l + 1], s = A.sub[l];
+        // zero rows around the dY2 image: before frame 0 and after frame s*To
+        lz_zero_rows<PREC>(imgg, 0, LZ_ZR);
+        lz_zero_rows<PREC>(imgg, LZ_ZR + s * To, LZ_ZR);
+        lz_publish();
+        // conv2^T over padded positions v = n - 16 of the Ti input frames, * act'(y1) -> imgg2
+        const int nfc = lz_nf(Ti + 16 + P);
+        LzChunk chk;
+        for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            const int vlo = max(n0 - 16, -P), vhi = min(n0 + 111, Ti + P - 1);
+            const int r0 = LZ_ZR + vlo + P - ks - 1;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgg, r0, vhi - vlo + ks + 2);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
+                rb[f] = LZ_ZR + v + P - r0;
+            }
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c2T(l), chk.last ? op_c1T(l) : op_c2T(l), WB, rb);
+            lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int F = chk.f0 + f - 1, t = 16 * F + c;   // frame of the column
+                if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
+                LzMask m;
+                m.load(mword(nb + 1 + 2 * l, F));
+                if (t < Ti)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        f32x4 v;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] * m.act(i, r, act);
+                        st4<PREC>(imgg2 + (size_t)(LZ_ZR + t) * GRB + (ch0 + 16 * i) * ESZ, v);
+                    }
+            }
+        }
+        lz_zero_rows<PREC>(imgg2, 0, LZ_ZR);
+        lz_zero_rows<PREC>(imgg2, LZ_ZR + Ti, LZ_ZR);
+        lz_publish();
+        // conv1^T (+ fold) + avg_pool^T of g(h_{l+1}) -> g(h_l); then the next dY: the dilated
+        // dY2 of block l-1 = g(h_l) * act'(y2_{l-1}), or g_pre0 = g(h_0) * act'(h0)
+        const int sp = l > 0 ? A.sub[l - 1] : 1;
+        const int mlayer = l > 0 ? nb + 2 + 2 * (l - 1) : nb;
+        char* nimg = l > 0 ? imgg : imgp;
+        float* gprev = gh[cur];
+        float* gnew = gh[cur ^ 1];
+        for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            const int vlo = max(n0 - 16, -P), vhi = min(n0 + 111, Ti + P - 1);
+            const int r0 = LZ_ZR + vlo + P - ks - 1;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgg2, r0, vhi - vlo + ks + 2);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
+                rb[f] = LZ_ZR + v + P - r0;
+            }
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            const AOp nxt = chk.last ? (l > 0 ? op_c2T(l - 1) : op_inTx()) : op_c1T(l);
+            if (chk.last && l == 0) {
+                // the bank phase runs on a 5-tile ring: refill the 2-tile ring with a dummy
+                fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), op_c1T(l), WB, rb);
+            } else {
+                fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), nxt, WB, rb);
+            }
+            lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int F = chk.f0 + f - 1, t = 16 * F + c;
+                if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
+                LzMask m;
+                m.load(mword(mlayer, F));
+                if (t < Ti)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        // torch avg_pool backward: grad / divide_factor (2, or 1 for a ceil tail)
+                        f32x4 gp;
+                        if (s == 2) {
+                            const int tp = t >> 1;
+                            const f32x4 g = l == nblk - 1 ? gN[i] : *lz_fl(gprev, tp, w, i);
+                            gp = (2 * tp + 1 < Ti) ? g / 2.f : g;
+                        } else {
+                            gp = l == nblk - 1 ? gN[i] : *lz_fl(gprev, t, w, i);
+                        }
+                        const f32x4 g = acc[i][f] + gp;
+                        if (l > 0) *lz_fl(gnew, t, w, i) = g;
+                        f32x4 v;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = g[r] * m.act(i, r, act);
+                        st4<PREC>(nimg + (size_t)(LZ_ZR + sp * t) * GRB + (ch0 + 16 * i) * ESZ, v);
+                        if (sp == 2)
+                            st4<PREC>(nimg + (size_t)(LZ_ZR + 2 * t + 1) * GRB + (ch0 + 16 * i) * ESZ,
+                                      f32x4{0.f, 0.f, 0.f, 0.f});
+                    }
+            }
+        }
+        cur ^= 1;
+    }
+
+    // ---- in_conv^T and conv bank^T (models.py:82-104, 337-338) chunk by chunk over the
+    // x-gradient's padded positions v = n - 4 (the bank's reflect pads are <= 4).  K of the
+    // bank^T split over waves: wave w sums over bank channels [32w, 32w+32) of every bank
+    // kernel into a partial g(x) [80][chunk]; g(b_k) for those channels is recomputed per
+    // chunk over the frames the chunk needs (in_conv^T, * act'(b_k)).
+    constexpr int CHF = LzBank<PREC>::CHF, CH = 16 * CHF;
+    constexpr int NFW = CHF + 1;                        // g(b_k) window: frames n0-16 .. n0+CH-1
+    constexpr int ZPB = 8;
+    ARing<5> ring5;
+    ring_fill(ring5, op_inTx());
+    lz_zero_rows<PREC>(imgp, 0, LZ_ZR);
+    lz_zero_rows<PREC>(imgp, LZ_ZR + T, LZ_ZR);
+    lz_publish();
+    char* GP = fz_lds;                                  // g_pre0 rows of frames n0-16 .. n0+CH-1
+    char* GBK = GP + NFW * 16 * RS;                     // per-wave g(b_k) slices, ZPB + NFW*16 + ZPB rows
+    static_assert((NFW * 16 + NFW * 16 + 2 * ZPB) * RS <= 150 * 1024, "bank windows overlap the fold scratch");
+    static_assert(2 * FZ_CIN * CH * 4 <= 150 * 1024, "reduction rows overlap the fold scratch");
+    float* R0 = reinterpret_cast<float*>(fz_lds);       // cross-wave partial sums (alias GP / GBK)
+    float* R1 = R0 + FZ_CIN * CH;
+    const int nfx = lz_nf(T + 8);
+    const AdamArgs& Ad = A.adam;
+    const float eps = A.scal[0];
+    const int step = min(max(*A.step, 1), A.table_len);
+    const float nstep = Ad.table[2 * (step - 1)];
+    const float bc2s = Ad.table[2 * (step - 1) + 1];
+    const float rbc2s = 1.f / bc2s;
+    const size_t xb = (size_t)b * FZ_CIN * T;
+    LzChunk chk;
+    for (int k = 0; lz_chunk(k, nfx, CHF, chk); ++k) {
+        const int n0 = 16 * chk.f0;
+        const int W0 = n0 - 16;                         // first frame of the g(b_k) window
+        __syncthreads();
+        lz_stage<PREC>(GP, imgp, LZ_ZR + W0, NFW * 16);
+        {   // this wave's slice of the GBK margins: zero
+            constexpr int V16 = 32 * ESZ / 16;
+            for (int idx = lane; idx < 2 * ZPB * V16; idx += 64) {
+                const int rr = idx / V16, part = idx - rr * V16;
+                const int row = rr < ZPB ? rr : NFW * 16 + rr;
+                *reinterpret_cast<f32x4*>(GBK + row * RS + 32 * w * ESZ + part * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        __syncthreads();
+        f32x4 accx[5][LZ_CHF];
+        zero_acc(accx);
+        // x passthrough of the cat: W_in[:, x block]^T g_pre0.  Pad columns read g_pre0 rows of
+        // frames outside [0, T), which are zero rows of the image: they get nothing.
+        int rbx[LZ_CHF];
+#pragma unroll
+        for (int f = 0; f < LZ_CHF; ++f) rbx[f] = min(max(n0 + 16 * f + c - 4, -4), T + 3) - W0;
+        if constexpr (CHF == LZ_CHF) {
+            fz_gemm<PREC, 5, LZ_CHF, FZ_C, 1>(accx, IC<LZ_CHF>{}, ring5, op_inTx(), op_inTb(0), GP, rbx);
+        } else {
+            fz_gemm<PREC, 5, LZ_CHF, FZ_C, 1>(accx, IC<CHF>{}, ring5, op_inTx(), op_inTb(0), GP, rbx);
+        }
+        for (int kb = 0; kb < nb; ++kb) {
+            const int kk = kb + 1, pl = kk / 2;
+            // g(b_k) for this wave's 32 bank channels over the window = (W_in[:, kb]^T g_pre0) * act'(b_k)
+            f32x4 acc[2][NFW];
+            zero_acc(acc);
+            int rt[NFW];
+#pragma unroll
+            for (int f = 0; f < NFW; ++f) rt[f] = 16 * f + c;
+            fz_gemm<PREC, 2, NFW, FZ_C, 1>(acc, IC<NFW>{}, ring5, op_inTb(kb), op_bankT(kb), GP, rt);
+#pragma unroll
+            for (int f = 0; f < NFW; ++f) {
+                const int F = W0 / 16 + f, u = 16 * F + c;
+                LzMask m;
+                if (F >= 0 && 16 * F < T) m.load(mword(kb, F));
+                else m.none();
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    f32x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = (u >= 0 && u < T) ? acc[i][f][r] * m.act(i, r, act) : 0.f;
+                    st4<PREC>(GBK + (ZPB + 16 * f + c) * RS + (ch0 + 16 * i) * ESZ, v);
+                }
+            }
+            __syncthreads();
+            // bank_k^T over this wave's channel quarter: rows u = v + pl - j of g(b_k)
+#pragma unroll
+            for (int f = 0; f < LZ_CHF; ++f) {
+                const int v = min(max(n0 + 16 * f + c - 4, -4), T + 3);
+                rb[f] = ZPB + (v + pl) - W0;
+            }
+            const AOp nxt = kb + 1 < nb ? op_inTb(kb + 1) : op_bankT(kb);
+            if constexpr (CHF == LZ_CHF) {
+                fz_gemm<PREC, 5, LZ_CHF, FZ_C, -1>(accx, IC<LZ_CHF>{}, ring5, op_bankT(kb), nxt, GBK, rb);
+            } else {
+                fz_gemm<PREC, 5, LZ_CHF, FZ_C, -1>(accx, IC<CHF>{}, ring5, op_bankT(kb), nxt, GBK, rb);
+            }
+            __syncthreads();
+        }
+        if (!chk.last) {   // ring5 now holds op_bankT(nb-1) prefetches; the next chunk starts at in_x^T
+            ring_fill(ring5, op_inTx());
+        }
+        lz_fold<5, CHF>(accx, chk.f0, 4, T, 4, FSCR);
+        // deterministic cross-wave sum ((p0 + p2) + (p1 + p3)) into R0 / R1 [80][CH]
+        for (int phase = 0; phase < 2; ++phase) {
+            if ((phase == 0) == (w >= 2)) {
+                float* R = (w & 1) ? R1 : R0;
+#pragma unroll
+                for (int i = 0; i < 5; ++i)
+#pragma unroll
+                    for (int f = 0; f < CHF; ++f)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float* p = R + (16 * i + 4 * kq + r) * CH + 16 * f + c;
+                            *p = phase ? accx[i][f][r] + *p : accx[i][f][r];
+                        }
+            }
+            __syncthreads();
+        }
+        // owned interior columns: t = n - 4 in [0, T)
+        for (int idx = tid; idx < FZ_CIN * CH; idx += 256) {
+            const int ci = idx / CH, col = idx - ci * CH;
+            const int n = n0 + col, t = n - 4;
+            if (!chk.owns(n) || t < 0 || t >= T) continue;
+            const float gsum = R0[ci * CH + col] + R1[ci * CH + col];
+            const size_t q = xb + (size_t)ci * T + t;
+            if (A.gx_out) {
+                A.gx_out[q] = gsum;
+                continue;
+            }
+            float p = Ad.ptb[q], mm = Ad.m[q], vv = Ad.v[q];
+            const float x = Ad.vc[q];
+            float g, ad;
+            if constexpr (PREC == PREC_F32) {
+                const float th = tanhf(p);
+                g = (gsum * eps) * (1.f - th * th);
+                mm = mm + Ad.b1c * (g - mm);
+                vv = vv * Ad.b2;
+                vv = vv + Ad.b2c * g * g;
+                p = p + nstep * (mm / (sqrtf(vv) / bc2s + Ad.adam_eps));
+                ad = x + eps * tanhf(p);
+            } else {
+                const float th = fast_tanh(p);
+                g = (gsum * eps) * (1.f - th * th);
+                mm = mm + Ad.b1c * (g - mm);
+                vv = vv * Ad.b2;
+                vv = vv + Ad.b2c * g * g;
+                const float den = __builtin_amdgcn_sqrtf(vv) * rbc2s + Ad.adam_eps;
+                p = p + nstep * (mm * __builtin_amdgcn_rcpf(den));
+                ad = x + eps * fast_tanh(p);
+            }
+            if (Ad.grad0 && step == 1) Ad.grad0[q] = g;
+            Ad.ptb[q] = p;
+            Ad.m[q] = mm;
+            Ad.v[q] = vv;
+            Ad.adv[q] = ad;
+        }
+    }
+}
+
+// LDS bytes of the long kernels (the host sets the same)
+constexpr int LZ_LDS_BYTES = 160 * 1024;
+
+#define AVC_LZ_INST(P)                                                    \
+    template __global__ void lz_se_fwd<P>(FusedArgs, LongArgs);          \
+    template __global__ void lz_se_bwd<P>(FusedArgs, LongArgs);
+AVC_LZ_INST(PREC_F32)
+AVC_LZ_INST(PREC_BF16)
+#undef AVC_LZ_INST
+
+}  // namespace avc

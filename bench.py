@@ -78,8 +78,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--cpu-procs", type=int, default=16,
-                    help="CPU baseline (ii): concurrent 1-thread processes (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-procs", type=int, default=12,
+                    help="CPU baseline (ii): concurrent 1-thread processes (the GPU box's CPU share is 16; "
+                         "its process guard allows 16 processes with the GPU open, this one included)")
     ap.add_argument("--cpu-worker", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: launcher + gloo rendezvous + sharding + timing, no attack computed")
@@ -193,7 +194,8 @@ def cpu_baseline_throughput(kind, budget_s, procs):
     throughput a CPU box gets from the reference), aggregated utts/s.  Child processes of
     this script (--cpu-worker), started with subprocess."""
     import subprocess
-    env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="",
+               CUDA_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.abspath(__file__), "--attack", kind, "--cpu-worker", str(budget_s)]
     ps = [subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, env=env)

@@ -220,15 +220,18 @@ int avc_dsp_profile_count(avc_dsp* dsp);
 int avc_dsp_profile_kernel(avc_dsp* dsp, int i, char* name, int name_len, long* launches, double* total_ms);
 
 /* Compute engine of a context.
- *  AUTO    (default): FUSED when the config and T allow it, else LAYERED.
+ *  AUTO    (default): FUSED for T <= 128, LONG above, when the config allows; else LAYERED.
  *  LAYERED: one implicit-GEMM launch per Conv1d / dgrad over the whole batch, activations in HBM
  *           (any SpeakerEncoder config, any T).
- *  FUSED  : one workgroup per utterance runs the whole conv stack out of LDS (3 launches per
+ *  FUSED  : one workgroup per utterance runs the whole conv stack out of LDS (2-3 launches per
  *           iteration); needs c_in=80, c_h=c_bank=c_out=128, bank_scale=1, bank_size<=8, odd
- *           kernel_size<=5, <=8 conv blocks with subsample 1|2, and T<=128 (else LAYERED).
- * avc_set_engine fails (non-zero) if FUSED is requested for a config that cannot use it;
+ *           kernel_size<=5, <=8 conv blocks with subsample 1|2, and T<=128 (above: LONG).
+ *  LONG   : the same per-utterance kernels family for any T: each layer runs over chunks of 128
+ *           frames staged through LDS, activations in per-utterance global scratch (the engine
+ *           for real 128-600-frame utterances; selectable at any T for cross-checks).
+ * avc_set_engine fails (non-zero) if FUSED / LONG is requested for a config that cannot use it;
  * avc_get_engine returns the engine a call with T frames would run on. */
-enum { AVC_ENGINE_AUTO = 0, AVC_ENGINE_LAYERED = 1, AVC_ENGINE_FUSED = 2 };
+enum { AVC_ENGINE_AUTO = 0, AVC_ENGINE_LAYERED = 1, AVC_ENGINE_FUSED = 2, AVC_ENGINE_LONG = 3 };
 int avc_set_engine(avc_ctx* ctx, int engine);
 int avc_get_engine(avc_ctx* ctx, int T);
 

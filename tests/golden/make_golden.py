@@ -134,8 +134,10 @@ def attack_fixture(au, attack_type, model, X, n_list, seeds, prefix, out, keep_l
 
 
 def make_inputs(B, T, seed):
+    """T: one length for all three inputs, or a dict {vc_src, vc_tgt, adv_tgt: frames}."""
     g = torch.Generator().manual_seed(seed)
-    return {k: torch.randn(B, 80, T, generator=g) for k in ("vc_src", "vc_tgt", "adv_tgt")}
+    lens = T if isinstance(T, dict) else {k: T for k in ("vc_src", "vc_tgt", "adv_tgt")}
+    return {k: torch.randn(B, 80, lens[k], generator=g) for k in ("vc_src", "vc_tgt", "adv_tgt")}
 
 
 def build(models, cfg):
@@ -150,6 +152,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--skip-1500", action="store_true")
+    ap.add_argument("--stage", default="all", choices=["all", "base", "long"],
+                    help="long: only the round-2 fixtures (T = 300 with three input lengths; "
+                         "e2e / fb at n = 100)")
     a = ap.parse_args()
     sys.dont_write_bytecode = True
     sys.path.insert(0, a.ref)
@@ -157,6 +162,11 @@ def main():
     import attack_utils as au  # noqa: E402
     torch.set_num_threads(os.cpu_count() or 1)
     seeds = [1000, 1001]
+
+    if a.stage in ("all", "long"):
+        long_fixtures(models, au, seeds)
+    if a.stage == "long":
+        return
 
     # ---------------- small config -------------------------------------------------
     for T in (32, 33):
@@ -214,6 +224,38 @@ def main():
         path = os.path.join(HERE, f"full_T{T}.npz")
         np.savez_compressed(path, **out)
         print("wrote", path, os.path.getsize(path))
+
+
+def long_fixtures(models, au, seeds):
+    """Round 2: real utterance lengths.  full_T300.npz -- vc_tgt 300 frames (the long
+    engine), vc_src 280 and adv_tgt 260 (every input its own length, as attack.py loads them):
+    emb / e2e / fb adv at n = 10, grad0, losses, SE(vc_tgt) and inference(vc_src, vc_tgt).
+    full_T128_n100.npz -- the e2e / fb attacks at n = 100 on full_T128's inputs."""
+    model = build(models, FULL_CFG)
+    hashes = {k: sha(v) for k, v in model.state_dict().items()}
+    X = make_inputs(2, {"vc_src": 280, "vc_tgt": 300, "adv_tgt": 260}, seed=300)
+    out = {"config": np.array(json.dumps(FULL_CFG)), "eps": np.float64(EPS), "T": np.int64(300),
+           "weight_sha256": np.array(json.dumps(hashes))}
+    for k, v in X.items():
+        out[k] = v.numpy()
+    with torch.no_grad():
+        out["se_vc_tgt"] = model.speaker_encoder(X["vc_tgt"]).numpy()
+        out["se_adv_tgt"] = model.speaker_encoder(X["adv_tgt"]).numpy()
+        out["inference"] = model.inference(X["vc_src"], X["vc_tgt"]).numpy()
+    for kind in ("emb", "e2e", "fb"):
+        attack_fixture(au, kind, model, X, [10], seeds, "", out, keep_losses=True)
+    path = os.path.join(HERE, "full_T300.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path))
+
+    X = make_inputs(2, 128, seed=128)              # full_T128.npz's inputs
+    out = {"config": np.array(json.dumps(FULL_CFG)), "eps": np.float64(EPS), "T": np.int64(128),
+           "weight_sha256": np.array(json.dumps(hashes))}
+    for kind in ("e2e", "fb"):
+        attack_fixture(au, kind, model, X, [100], seeds, "", out, keep_losses=True)
+    path = os.path.join(HERE, "full_T128_n100.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path))
 
 
 if __name__ == "__main__":

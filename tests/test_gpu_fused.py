@@ -33,7 +33,7 @@ def full(golden):
 def test_engine_selection(full, golden):
     z, m, ctx = full
     assert ctx.engine_for(128) == "fused" and ctx.engine_for(9) == "fused"
-    assert ctx.engine_for(129) == "layered"          # LDS images are sized for T <= 128
+    assert ctx.engine_for(129) == "long"             # LDS images are sized for T <= 128: chunked above
     small = model_from_fixture(golden("small_T32")).to(DEV)
     sctx = avc_native.context_for(small.speaker_encoder, DEV)
     assert sctx.engine_for(32) == "layered"          # c_h = 32: not the fused engine's shape

@@ -221,3 +221,25 @@ def test_lrelu_config(golden, kind):
     adv = oracle.attack(kind, w, cfg, z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 10, z[f"{kind}_ptb0"], record=rec)
     check_adv(adv, z[f"{kind}_adv_n10"], 10)
     assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= (TOL_GRAD_REL_VC if kind != "emb" else TOL_GRAD_REL)
+
+
+def test_long_mixed_lengths_fixture(golden):
+    """full_T300.npz (round 2): vc_src 280, vc_tgt 300, adv_tgt 260 frames, made by the
+    reference itself: the oracle's SE / inference and its emb / e2e / fb attacks (n = 10)
+    at these lengths."""
+    z = golden("full_T300")
+    w = oracle_weights(model_from_fixture(z))
+    cfg = cfg_of(z)
+    assert z["vc_src"].shape[2] == 280 and z["vc_tgt"].shape[2] == 300 and z["adv_tgt"].shape[2] == 260
+    e, _ = oracle.se_forward(w, cfg["SpeakerEncoder"], z["vc_tgt"])
+    assert rel(e, z["se_vc_tgt"]) <= TOL_SE_REL
+    out = oracle.inference(w, cfg, z["vc_src"], z["vc_tgt"])
+    assert out.shape == z["inference"].shape and rel(out, z["inference"]) <= 1e-5
+    for kind in ("emb", "e2e", "fb"):
+        rec = {}
+        fn = getattr(oracle, f"{kind}_attack")
+        args = (z["vc_tgt"], z["adv_tgt"]) if kind == "emb" else (z["vc_src"], z["vc_tgt"], z["adv_tgt"])
+        adv = fn(w, cfg, *args, 0.1, 10, z[f"{kind}_ptb0"], record=rec)
+        check_adv(adv, z[f"{kind}_adv_n10"], 10)
+        assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= (TOL_GRAD_REL if kind == "emb" else TOL_GRAD_REL_VC)
+        np.testing.assert_allclose(rec["losses"], z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
