@@ -35,6 +35,10 @@ template <int PREC>
 __global__ void lz_se_fwd(FusedArgs A, LongArgs L);
 template <int PREC>
 __global__ void lz_se_bwd(FusedArgs A, LongArgs L);
+template <int PREC>
+__global__ void lz_dec_fwd(DecArgs A, LongArgs L);
+template <int PREC>
+__global__ void lz_dec_bwd(DecArgs A, LongArgs L);
 template <int PREC, int SH>
 __global__ void dec_fwd_fused(DecArgs A);
 template <int PREC, int SH>
@@ -83,7 +87,9 @@ struct HostConv {
     const float* b;
 };
 
-enum LaunchKind { L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD, L_DZ_FWD, L_DZ_BWD, L_DENSE, L_LZ_FWD, L_LZ_BWD };
+enum LaunchKind {
+    L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD, L_DZ_FWD, L_DZ_BWD, L_DENSE, L_LZ_FWD, L_LZ_BWD, L_LZD_FWD, L_LZD_BWD
+};
 constexpr size_t LZ_SHMEM = 160 * 1024;   // the long kernels use the whole LDS (avc_long.hip)
 
 // conv_gemm instantiations (avc_gemm_variants.h); the planner autotunes one per
@@ -430,7 +436,9 @@ static int set_fused_attrs() {
 #undef AVC_FZ_FNS
     for (auto& fn : fns) HIPCHK(hipFuncSetAttribute(fn.first, hipFuncAttributeMaxDynamicSharedMemorySize, fn.second));
     for (const void* fn : {(const void*)lz_se_fwd<PREC_F32>, (const void*)lz_se_fwd<PREC_BF16>,
-                           (const void*)lz_se_bwd<PREC_F32>, (const void*)lz_se_bwd<PREC_BF16>})
+                           (const void*)lz_se_bwd<PREC_F32>, (const void*)lz_se_bwd<PREC_BF16>,
+                           (const void*)lz_dec_fwd<PREC_F32>, (const void*)lz_dec_fwd<PREC_BF16>,
+                           (const void*)lz_dec_bwd<PREC_F32>, (const void*)lz_dec_bwd<PREC_BF16>})
         HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LZ_SHMEM));
     return 0;
 }
@@ -1473,6 +1481,14 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
     case L_LZ_BWD:
         if (L.prec == PREC_F32) klaunch(ev, false, lz_se_bwd<PREC_F32>, L.grid, L.block, L.shmem, s, L.fz, L.lz);
         else klaunch(ev, false, lz_se_bwd<PREC_BF16>, L.grid, L.block, L.shmem, s, L.fz, L.lz);
+        return hipGetLastError();
+    case L_LZD_FWD:
+        if (L.prec == PREC_F32) klaunch(ev, false, lz_dec_fwd<PREC_F32>, L.grid, L.block, L.shmem, s, L.dz, L.lz);
+        else klaunch(ev, false, lz_dec_fwd<PREC_BF16>, L.grid, L.block, L.shmem, s, L.dz, L.lz);
+        return hipGetLastError();
+    case L_LZD_BWD:
+        if (L.prec == PREC_F32) klaunch(ev, false, lz_dec_bwd<PREC_F32>, L.grid, L.block, L.shmem, s, L.dz, L.lz);
+        else klaunch(ev, false, lz_dec_bwd<PREC_BF16>, L.grid, L.block, L.shmem, s, L.dz, L.lz);
         return hipGetLastError();
     default:
         return hipErrorInvalidValue;

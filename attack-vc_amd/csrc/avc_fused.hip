@@ -907,6 +907,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const float nstep = Ad.table[2 * (step - 1)];
     const float bc2s = Ad.table[2 * (step - 1) + 1];
     const float rbc2s = 1.f / bc2s;
+    const AdamStep S{nstep, bc2s, rbc2s, eps};
     const size_t base4 = (size_t)b * FZ_CIN * T / 4;
     f32x4* __restrict__ ptb4 = reinterpret_cast<f32x4*>(Ad.ptb) + base4;
     f32x4* __restrict__ m4 = reinterpret_cast<f32x4*>(Ad.m) + base4;
@@ -948,27 +949,13 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 p[e] = p[e] + nstep * (mm[e] * (vv[e] * bc2s + Ad.adam_eps));
                 ad[e] = X[k][e] + eps * p[e] * 0.25f;
 #else
-                if constexpr (PREC == PREC_F32) {
-                    // fp32 mode: torch's IEEE arithmetic (tanh, sqrt(v) / sqrt(bc2) + eps, m / den;
-                    // _single_tensor_adam, torch/optim/adam.py:531-547)
-                    const float th = tanhf(p[e]);
-                    g[e] = (gsum[e] * eps) * (1.f - th * th);
-                    mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
-                    vv[e] = vv[e] * Ad.b2;
-                    vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
-                    p[e] = p[e] + nstep * (mm[e] / (sqrtf(vv[e]) / bc2s + Ad.adam_eps));
-                    ad[e] = X[k][e] + eps * tanhf(p[e]);
-                } else {
-                    // bf16 mode: hardware exp2 / rcp / sqrt (the tail is VALU-bound at one wave per SIMD)
-                    const float th = fast_tanh(p[e]);
-                    g[e] = (gsum[e] * eps) * (1.f - th * th);
-                    mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
-                    vv[e] = vv[e] * Ad.b2;
-                    vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
-                    const float den = __builtin_amdgcn_sqrtf(vv[e]) * rbc2s + Ad.adam_eps;
-                    p[e] = p[e] + nstep * (mm[e] * __builtin_amdgcn_rcpf(den));
-                    ad[e] = X[k][e] + eps * fast_tanh(p[e]);
-                }
+                float pe = p[e], me = mm[e], ve = vv[e], ge, ae;
+                adam_elem<PREC>(Ad, S, gsum[e], X[k][e], pe, me, ve, ge, ae);
+                p[e] = pe;
+                mm[e] = me;
+                vv[e] = ve;
+                g[e] = ge;
+                ad[e] = ae;
 #endif
             }
             if (g04) g04[q] = g;

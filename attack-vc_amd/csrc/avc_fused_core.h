@@ -446,6 +446,38 @@ __device__ __forceinline__ float fast_tanh(float x) {
     return a < 0.625f ? small : big;
 }
 
+// One element of the Adam tail (attack_utils.py:78-86, torch _single_tensor_adam): tanh'
+// of the reparameterisation, Adam moments and step, next adv = vc + eps*tanh(ptb).  One
+// definition for every engine, with the contraction pinned, so the fused and long engines
+// round identically (the compiler otherwise contracts vector and scalar copies differently).
+//   fp32 mode: torch's per-operation IEEE arithmetic (tanhf, sqrt(v) / sqrt(bc2) + eps, m / den)
+//   bf16 mode: hardware exp2 / rcp / sqrt and explicit fmas (the tail is VALU-bound)
+struct AdamStep {
+    float nstep, bc2s, rbc2s, eps;
+};
+template <int PREC>
+__device__ __forceinline__ void adam_elem(const AdamArgs& Ad, const AdamStep& S, float gsum, float x, float& p,
+                                          float& mm, float& vv, float& g, float& ad) {
+#pragma clang fp contract(off)
+    if constexpr (PREC == PREC_F32) {
+        const float th = tanhf(p);
+        g = (gsum * S.eps) * (1.f - th * th);
+        mm = mm + Ad.b1c * (g - mm);
+        vv = vv * Ad.b2;
+        vv = vv + Ad.b2c * g * g;
+        p = p + S.nstep * (mm / (sqrtf(vv) / S.bc2s + Ad.adam_eps));
+        ad = x + S.eps * tanhf(p);
+    } else {
+        const float th = fast_tanh(p);
+        g = (gsum * S.eps) * __builtin_fmaf(-th, th, 1.f);
+        mm = __builtin_fmaf(Ad.b1c, g - mm, mm);
+        vv = __builtin_fmaf(Ad.b2c * g, g, vv * Ad.b2);
+        const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(vv), S.rbc2s, Ad.adam_eps);
+        p = __builtin_fmaf(S.nstep, mm * __builtin_amdgcn_rcpf(den), p);
+        ad = __builtin_fmaf(S.eps, fast_tanh(p), x);
+    }
+}
+
 // write 4 consecutive channels of frame t of a padded operand image (pad P rows each
 // side, reflect): row P+t, plus its mirror rows (F.pad reflect)
 template <int PREC>

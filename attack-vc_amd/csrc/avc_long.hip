@@ -767,6 +767,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     const float nstep = Ad.table[2 * (step - 1)];
     const float bc2s = Ad.table[2 * (step - 1) + 1];
     const float rbc2s = 1.f / bc2s;
+    const AdamStep S{nstep, bc2s, rbc2s, eps};
     const size_t xb = (size_t)b * FZ_CIN * T;
     LzChunk chk;
     for (int k = 0; lz_chunk(k, nfx, CHF, chk); ++k) {
@@ -865,26 +866,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                 continue;
             }
             float p = Ad.ptb[q], mm = Ad.m[q], vv = Ad.v[q];
-            const float x = Ad.vc[q];
             float g, ad;
-            if constexpr (PREC == PREC_F32) {
-                const float th = tanhf(p);
-                g = (gsum * eps) * (1.f - th * th);
-                mm = mm + Ad.b1c * (g - mm);
-                vv = vv * Ad.b2;
-                vv = vv + Ad.b2c * g * g;
-                p = p + nstep * (mm / (sqrtf(vv) / bc2s + Ad.adam_eps));
-                ad = x + eps * tanhf(p);
-            } else {
-                const float th = fast_tanh(p);
-                g = (gsum * eps) * (1.f - th * th);
-                mm = mm + Ad.b1c * (g - mm);
-                vv = vv * Ad.b2;
-                vv = vv + Ad.b2c * g * g;
-                const float den = __builtin_amdgcn_sqrtf(vv) * rbc2s + Ad.adam_eps;
-                p = p + nstep * (mm * __builtin_amdgcn_rcpf(den));
-                ad = x + eps * fast_tanh(p);
-            }
+            adam_elem<PREC>(Ad, S, gsum, Ad.vc[q], p, mm, vv, g, ad);
             if (Ad.grad0 && step == 1) Ad.grad0[q] = g;
             Ad.ptb[q] = p;
             Ad.m[q] = mm;
@@ -894,12 +877,532 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Decoder (models.py:403-435) for any length: forward (+ e2e loss) and backward to
+// d loss / d [mean | std] of every AdaIN (dec_fwd_fused / dec_bwd_fused in avc_vc.hip for
+// the T <= 128 engine).  InstanceNorm statistics span all chunks: a layer's GEMM writes its
+// raw output (+ bias) as an fp32 fragment-layout stream and accumulates the row sums over
+// the columns each chunk owns; a second pass takes the centred second moment, a third
+// normalises (AdaIN, act, residual) into the next operand image.  A x2 pixel-shuffle conv
+// runs as two half-GEMMs over the even / odd output channels of one staged window: half s
+// of channel c is frame 2t + s of the shuffled output (models.py:33-49).
+// LongArgs: img[0] block input (h), img[1] conv1 output / dY images, img[2] second dY image,
+// fl[0], fl[1] residual stream / its gradient (ping-pong), fl[2] raw / temporary gradients.
+// The forward stashes each InstanceNorm's normalised output (fp32, fragment layout over
+// the layer's frames, at stash + stash_off[q]) and 1/std for the backward.
+// ---------------------------------------------------------------------------------
+
+// [C][T] fp32 (a [B][C][T] tensor's utterance) -> image rows LZ_ZR + t, channels [0, C)
+template <int PREC, int C>
+__device__ __forceinline__ void lz_ct_to_img(char* img, const float* src, int T) {
+    using Z = Lz<PREC>;
+    constexpr int VE = 16 / Z::ESZ, NG = C / VE;
+    for (int idx = threadIdx.x; idx < NG * T; idx += 256) {
+        const int g = idx / T, t = idx - g * T;
+        f32x4 v;
+        if constexpr (PREC == PREC_F32) {
+            v = f32x4{src[(size_t)(4 * g) * T + t], src[(size_t)(4 * g + 1) * T + t], src[(size_t)(4 * g + 2) * T + t],
+                      src[(size_t)(4 * g + 3) * T + t]};
+        } else {
+            bf16x8 h;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) h[e] = (__bf16)src[(size_t)(8 * g + e) * T + t];
+            v = __builtin_bit_cast(f32x4, h);
+        }
+        *reinterpret_cast<f32x4*>(img + (size_t)(LZ_ZR + t) * Z::GRB + 16 * g) = v;
+    }
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
+    using Z = Lz<PREC>;
+    constexpr int RS = Z::RS, ESZ = Z::ESZ;
+    constexpr int VE = 16 / ESZ, KS = 4 * VE;
+    constexpr int NF = LZ_CHF;
+    const int b = blockIdx.x;
+    const int nblk = A.nblk, ks = A.ks, P = ks / 2, act = A.act;
+    const int T0 = A.Tl[0], Tn = A.Tl[nblk];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, kq = lane >> 4;
+    const int ch0 = 32 * w + 4 * kq;
+    const float* cond = A.cond + (size_t)b * (2 * nblk) * 256;
+    const bool stash = A.stash_per_utt > 0;
+    float* stb = A.stash + (size_t)b * A.stash_per_utt;
+
+    char* imgh = L.img[0] + (size_t)b * L.img_stride;
+    char* imgy = L.img[1] + (size_t)b * L.img_stride;
+    float* hf[2] = {L.fl[0] + (size_t)b * L.fl_stride, L.fl[1] + (size_t)b * L.fl_stride};
+    float* raw = L.fl[2] + (size_t)b * L.fl_stride;
+
+    const int ns_c = ks * FZ_C / KS;
+    const int ns_1 = FZ_C / KS;
+    auto op_in = [&]() __attribute__((always_inline)) { return aop(A.w.in, 2 * w, 2, ns_1, ns_1); };
+    auto op_c1 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2 = [&](int l, int s) __attribute__((always_inline)) { return aop(A.w.c2[l][s], 2 * w, 2, ns_c, ns_c); };
+    // out_conv: 80 rows = 5 tiles; waves take tiles {0,1}, {2,3}, {3,4}, {3,4}
+    auto op_out = [&]() __attribute__((always_inline)) { return aop(A.w.out, w < 2 ? 2 * w : 3, 2, ns_1, ns_1); };
+    ARing<2> ring;
+    ring_fill(ring, op_in());
+    int rb[NF];
+    char* WB = fz_lds;
+    f32x4 in_s[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+
+    lz_ct_to_img<PREC, FZ_C>(imgy, A.mu + (size_t)b * FZ_C * T0, T0);   // mu -> in_conv operand
+    lz_publish();
+    // in_conv (1x1) + b -> raw
+    {
+        f32x4 bi[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) bi[i] = *reinterpret_cast<const f32x4*>(A.w.b_in + ch0 + 16 * i);
+        LzChunk chk;
+        for (int k = 0; lz_chunk(k, lz_nf(T0), NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgy, LZ_ZR + n0, 129);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T0 - 1) - n0;
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_in(), chk.last ? op_c1(0) : op_in(), WB, rb);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = n0 + 16 * f + c;
+                if (t < T0 && chk.owns(t))
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const f32x4 y = acc[i][f] + bi[i];
+                        *lz_fl(raw, t, w, i) = y;
+                        in_s[i] += y;
+                    }
+            }
+        }
+    }
+    // InstanceNorm over the Tl frames of raw, then out(t, i, yhat, invstd)
+    auto in_pass = [&](int Tl, auto&& out) __attribute__((always_inline)) {
+        lz_publish();
+        f32x4 mean[2], inv[2];
+        lz_in_stats(raw, Tl, w, in_s, mean, inv);
+        for (int F = 0; F < lz_nf(Tl); ++F) {
+            const int t = 16 * F + c;
+            if (t < Tl)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) out(t, i, (*lz_fl(raw, t, w, i) - mean[i]) * inv[i], inv[i]);
+        }
+        in_s[0] = in_s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto put_inv = [&](int q, const f32x4& inv, int i) __attribute__((always_inline)) {
+        if (stash && c == 0)
+            *reinterpret_cast<f32x4*>(A.invstd + ((size_t)b * 2 * nblk + q) * 128 + ch0 + 16 * i) = inv;
+    };
+    in_pass(T0, [&](int t, int i, f32x4 v, f32x4) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_f(v[r], act);
+        *lz_fl(hf[0], t, w, i) = v;
+        lz_put<PREC>(imgh, t, T0, (ch0 + 16 * i) * ESZ, v);
+    });
+
+    int cur = 0;
+    for (int l = 0; l < nblk; ++l) {
+        const int Ti = A.Tl[l], up = A.up[l], To = Ti * up;
+        f32x4 b1[2], b2[2][2], mn1[2], sd1[2], mn2[2], sd2[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            b1[i] = *reinterpret_cast<const f32x4*>(A.w.b_c1[l] + ch0 + 16 * i);
+            b2[0][i] = *reinterpret_cast<const f32x4*>(A.w.b_c2[l][0] + ch0 + 16 * i);
+            b2[1][i] = *reinterpret_cast<const f32x4*>(A.w.b_c2[l][1] + ch0 + 16 * i);
+            mn1[i] = *reinterpret_cast<const f32x4*>(cond + (2 * l) * 256 + ch0 + 16 * i);
+            sd1[i] = *reinterpret_cast<const f32x4*>(cond + (2 * l) * 256 + 128 + ch0 + 16 * i);
+            mn2[i] = *reinterpret_cast<const f32x4*>(cond + (2 * l + 1) * 256 + ch0 + 16 * i);
+            sd2[i] = *reinterpret_cast<const f32x4*>(cond + (2 * l + 1) * 256 + 128 + ch0 + 16 * i);
+        }
+        lz_publish();
+        // conv1 -> raw -> IN -> AdaIN(2l) -> act -> imgy
+        LzChunk chk;
+        const int nfi = lz_nf(Ti);
+        for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgh, LZ_ZR + n0 - P, 127 + ks + 2);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Ti - 1) - n0;
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c1(l), chk.last ? op_c2(l, 0) : op_c1(l), WB, rb);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = n0 + 16 * f + c;
+                if (t < Ti && chk.owns(t))
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const f32x4 y = acc[i][f] + b1[i];
+                        *lz_fl(raw, t, w, i) = y;
+                        in_s[i] += y;
+                    }
+            }
+        }
+        float* st1 = stb + A.stash_off[2 * l];
+        in_pass(Ti, [&](int t, int i, f32x4 yh, f32x4 inv) __attribute__((always_inline)) {
+            if (stash) *lz_fl(st1, t, w, i) = yh;
+            if (t == c) put_inv(2 * l, inv, i);
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = act_f(yh[r] * sd1[i][r] + mn1[i][r], act);
+            lz_put<PREC>(imgy, t, Ti, (ch0 + 16 * i) * ESZ, v);
+        });
+        lz_publish();
+        // conv2 (up = 1: one GEMM; up = 2: the even / odd half-GEMMs) -> raw over To frames
+        const AOp nxt = l + 1 < nblk ? op_c1(l + 1) : op_out();
+        for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgy, LZ_ZR + n0 - P, 127 + ks + 2);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Ti - 1) - n0;
+            for (int s = 0; s < up; ++s) {
+                f32x4 acc[2][NF];
+                zero_acc(acc);
+                const AOp nx = s + 1 < up ? op_c2(l, 1) : (chk.last ? nxt : op_c2(l, 0));
+                fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l, s), nx, WB, rb);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const int t = n0 + 16 * f + c;
+                    if (t < Ti && chk.owns(t))
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) {
+                            const f32x4 y = acc[i][f] + b2[s][i];
+                            *lz_fl(raw, up * t + s, w, i) = y;
+                            in_s[i] += y;
+                        }
+                }
+            }
+        }
+        float* st2 = stb + A.stash_off[2 * l + 1];
+        float* hin = hf[cur];
+        float* hout = hf[cur ^ 1];
+        // IN over the To frames -> AdaIN(2l+1) -> act -> + (nearest-upsampled) residual
+        in_pass(To, [&](int t, int i, f32x4 yh, f32x4 inv) __attribute__((always_inline)) {
+            if (stash) *lz_fl(st2, t, w, i) = yh;
+            if (t == c) put_inv(2 * l + 1, inv, i);
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = act_f(yh[r] * sd2[i][r] + mn2[i][r], act);
+            const f32x4 h = v + *lz_fl(hin, up == 2 ? t >> 1 : t, w, i);
+            *lz_fl(hout, t, w, i) = h;
+            lz_put<PREC>(imgh, t, To, (ch0 + 16 * i) * ESZ, h);
+        });
+        cur ^= 1;
+    }
+    lz_publish();
+    // out_conv (1x1, 128 -> 80) + b -> out [80][Tn]; e2e: MSE(out, tgt) - 0.1 MSE(out, org)
+    // (attack_utils.py:41-43), its gradient and the per-utterance loss
+    const bool e2e = A.tgt_out != nullptr;
+    const float gscale = e2e ? A.scal[2] : 0.f;
+    float q1 = 0.f, q2 = 0.f;
+    float* OS = reinterpret_cast<float*>(fz_lds + 80 * 1024);   // [80][128] fp32 chunk of out
+    const int tile0 = w < 2 ? 2 * w : 3;
+    LzChunk chk;
+    for (int k = 0; lz_chunk(k, lz_nf(Tn), NF, chk); ++k) {
+        const int n0 = 16 * chk.f0;
+        __syncthreads();
+        lz_stage<PREC>(WB, imgh, LZ_ZR + n0, 129);
+        __syncthreads();
+#pragma unroll
+        for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Tn - 1) - n0;
+        f32x4 acc[2][NF];
+        zero_acc(acc);
+        fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_out(), op_out(), WB, rb);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int tile = tile0 + i;
+            const bool mine = w < 2 || (w == 2 && i == 1);
+            if (!mine) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = 16 * tile + 4 * kq + r;
+                const float bo = A.w.b_out[co];
+#pragma unroll
+                for (int f = 0; f < NF; ++f) OS[co * 128 + 16 * f + c] = acc[i][f][r] + bo;
+            }
+        }
+        __syncthreads();
+        float* outb = A.out + (size_t)b * DZ_COUT * Tn;
+        for (int idx = tid; idx < DZ_COUT * 128; idx += 256) {
+            const int co = idx >> 7, col = idx & 127;
+            const int t = n0 + col;
+            if (t >= Tn || !chk.owns(t)) continue;
+            const float o = OS[idx];
+            const size_t q = (size_t)co * Tn + t;
+            outb[q] = o;
+            if (e2e) {
+                const size_t qb = (size_t)b * DZ_COUT * Tn + q;
+                const float d1 = o - A.tgt_out[qb], d2 = o - A.org_out[qb];
+                A.g_out[qb] = gscale * d1 + gscale * d2 * -0.1f;
+                q1 += d1 * d1;
+                q2 += d2 * d2;
+            }
+        }
+    }
+    if (e2e && A.losses) {
+        // per-utterance loss: wave partial sums (fixed butterfly) then a fixed-order sum
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            q1 += __shfl_xor(q1, o);
+            q2 += __shfl_xor(q2, o);
+        }
+        float* lsum = reinterpret_cast<float*>(fz_lds + 150 * 1024);
+        __syncthreads();
+        if (lane == 0) {
+            lsum[2 * w] = q1;
+            lsum[2 * w + 1] = q2;
+        }
+        __syncthreads();
+        const int step = *A.step;
+        if (tid == 0 && step >= 1 && step <= A.loss_len) {
+            const float n = (float)(DZ_COUT * Tn);
+            const float s1 = (lsum[0] + lsum[2]) + (lsum[4] + lsum[6]);
+            const float s2 = (lsum[1] + lsum[3]) + (lsum[5] + lsum[7]);
+            A.losses[(size_t)(step - 1) * A.B + b] = s1 / n - 0.1f * (s2 / n);
+        }
+    }
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
+    using Z = Lz<PREC>;
+    constexpr int RS = Z::RS, ESZ = Z::ESZ, GRB = Z::GRB;
+    constexpr int VE = 16 / ESZ, KS = 4 * VE;
+    constexpr int NF = LZ_CHF;
+    const int b = blockIdx.x;
+    const int nblk = A.nblk, ks = A.ks, P = ks / 2, act = A.act;
+    const int Tn = A.Tl[nblk];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 15, kq = lane >> 4;
+    const int ch0 = 32 * w + 4 * kq;
+    const float* cond = A.cond + (size_t)b * (2 * nblk) * 256;
+    float* gcond = A.g_cond + (size_t)b * (2 * nblk) * 256;
+    const float* stb = A.stash + (size_t)b * A.stash_per_utt;
+
+    char* imgg = L.img[1] + (size_t)b * L.img_stride;    // dY image (half 0), the out_conv^T operand
+    char* imgg2 = L.img[2] + (size_t)b * L.img_stride;   // dY image of half 1
+    float* gh[2] = {L.fl[0] + (size_t)b * L.fl_stride, L.fl[1] + (size_t)b * L.fl_stride};
+    float* tmp = L.fl[2] + (size_t)b * L.fl_stride;
+    float* FSCR = reinterpret_cast<float*>(fz_lds + 150 * 1024) + w * (5 * 16 * 8);
+
+    const int ns_c = ks * FZ_C / KS;
+    const int ns_o = (DZ_COUT + KS - 1) / KS;
+    auto op_outT = [&]() __attribute__((always_inline)) { return aop(A.w.outT, 2 * w, 2, ns_o, ns_o); };
+    auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
+    auto op_c2T = [&](int l, int s) __attribute__((always_inline)) { return aop(A.w.c2T[l][s], 2 * w, 2, ns_c, ns_c); };
+    ARing<2> ring;
+    ring_fill(ring, op_outT());
+    int rb[NF];
+    char* WB = fz_lds;
+
+    // g_in [80][Tn] -> image (channels 80..127 of each row zero: the K padding of out_conv^T)
+    lz_zero_rows<PREC>(imgg, 0, LZ_ZR + Tn + 2 * LZ_ZR);
+    lz_publish();
+    lz_ct_to_img<PREC, DZ_COUT>(imgg, A.g_in + (size_t)b * DZ_COUT * Tn, Tn);
+    lz_publish();
+    // g(h_N) = out_conv^T g_out -> gh[0]
+    {
+        LzChunk chk;
+        for (int k = 0; lz_chunk(k, lz_nf(Tn), NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgg, LZ_ZR + n0, 130);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Tn - 1) - n0;
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, DZ_COUT, 1>(acc, IC<NF>{}, ring, op_outT(),
+                                            chk.last ? op_c2T(nblk - 1, 0) : op_outT(), WB, rb);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = n0 + 16 * f + c;
+                if (t < Tn && chk.owns(t))
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) *lz_fl(gh[0], t, w, i) = acc[i][f];
+            }
+        }
+    }
+    // act + AdaIN + InstanceNorm backward of IN layer q over Tl frames (models.py:66-79, 176):
+    //   z = yhat*std + mean, g_z = g * act'(z);  d/dmean = sum g_z,  d/dstd = sum g_z yhat;
+    //   d/dx = invstd std (g_z - (sum g_z)/n - yhat (sum g_z yhat)/n).
+    // gsrc(t, i) -> g; pass 1 keeps g_z in tmp and writes d/d cond[q]; pass 2 hands
+    // (t, i, d/dx) to out.
+    auto adain_in_bwd = [&](int q, int Tl, auto&& gsrc, auto&& out) __attribute__((always_inline)) {
+        const float* yq = stb + A.stash_off[q];
+        f32x4 mn[2], sd[2], is[2], gm[2], gs[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            mn[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
+            sd[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
+            is[i] = *reinterpret_cast<const f32x4*>(A.invstd + ((size_t)b * 2 * nblk + q) * 128 + ch0 + 16 * i);
+            gm[i] = gs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        lz_publish();
+        for (int F = 0; F < lz_nf(Tl); ++F) {
+            const int t = 16 * F + c;
+            if (t < Tl)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const f32x4 g = gsrc(t, i);
+                    const f32x4 yh = *lz_fl(const_cast<float*>(yq), t, w, i);
+                    f32x4 z;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) z[r] = g[r] * act_d(yh[r] * sd[i][r] + mn[i][r], act);
+                    *lz_fl(tmp, t, w, i) = z;
+                    gm[i] += z;
+                    gs[i] += z * yh;
+                }
+        }
+        f32x4 k1[2], k2[2], k3[2];
+        const float inv_n = 1.f / (float)Tl;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            row16_sum(gm[i]);
+            row16_sum(gs[i]);
+            if (c == 0) {
+                *reinterpret_cast<f32x4*>(gcond + q * 256 + ch0 + 16 * i) = gm[i];
+                *reinterpret_cast<f32x4*>(gcond + q * 256 + 128 + ch0 + 16 * i) = gs[i];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                k1[i][r] = is[i][r] * sd[i][r];
+                k2[i][r] = gm[i][r] * inv_n;
+                k3[i][r] = gs[i][r] * inv_n;
+            }
+        }
+        lz_publish();
+        for (int F = 0; F < lz_nf(Tl); ++F) {
+            const int t = 16 * F + c;
+            if (t < Tl)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const f32x4 z = *lz_fl(tmp, t, w, i);
+                    const f32x4 yh = *lz_fl(const_cast<float*>(yq), t, w, i);
+                    f32x4 d;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) d[r] = k1[i][r] * (z[r] - k2[i][r] - yh[r] * k3[i][r]);
+                    out(t, i, d);
+                }
+        }
+    };
+
+    int cur = 0;
+    for (int l = nblk - 1; l >= 0; --l) {
+        const int Ti = A.Tl[l], up = A.up[l], To = Ti * up;
+        float* gin = gh[cur];            // g(h_{l+1}) over To frames
+        float* gout = gh[cur ^ 1];       // g(h_l) over Ti frames
+        // conv2 branch: act, AdaIN(2l+1), IN backward over To frames -> dY image(s): frame
+        // 2t + s of the shuffled output is half s of frame t
+        adain_in_bwd(2 * l + 1, To, [&](int t, int i) __attribute__((always_inline)) { return *lz_fl(gin, t, w, i); },
+                     [&](int t, int i, f32x4 d) __attribute__((always_inline)) {
+                         char* im = (up == 2 && (t & 1)) ? imgg2 : imgg;
+                         const int tt = up == 2 ? t >> 1 : t;
+                         st4<PREC>(im + (size_t)(LZ_ZR + tt) * GRB + (ch0 + 16 * i) * ESZ, d);
+                     });
+        lz_zero_rows<PREC>(imgg, 0, LZ_ZR);
+        lz_zero_rows<PREC>(imgg, LZ_ZR + Ti, LZ_ZR);
+        if (up == 2) {
+            lz_zero_rows<PREC>(imgg2, 0, LZ_ZR);
+            lz_zero_rows<PREC>(imgg2, LZ_ZR + Ti, LZ_ZR);
+        }
+        lz_publish();
+        // conv2^T (both halves) over padded positions of the Ti frames -> tmp (g of conv1's output)
+        const int nfc = lz_nf(Ti + 16 + P);
+        LzChunk chk;
+        for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            const int vlo = max(n0 - 16, -P), vhi = min(n0 + 111, Ti + P - 1);
+            const int r0 = LZ_ZR + vlo + P - ks - 1;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
+                rb[f] = LZ_ZR + v + P - r0;
+            }
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            for (int s = 0; s < up; ++s) {
+                __syncthreads();
+                lz_stage<PREC>(WB, s ? imgg2 : imgg, r0, vhi - vlo + ks + 2);
+                __syncthreads();
+                const AOp nx = s + 1 < up ? op_c2T(l, 1) : (chk.last ? (l > 0 ? op_c1T(l) : op_c2T(l, 0)) : op_c2T(l, 0));
+                fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c2T(l, s), nx, WB, rb);
+            }
+            lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int F = chk.f0 + f - 1, t = 16 * F + c;
+                if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
+                if (t < Ti)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) *lz_fl(gout, t, w, i) = acc[i][f];   // scratch: g of conv1's output
+            }
+        }
+        // conv1 branch: act, AdaIN(2l), IN backward -> dY of conv1 (the first block stops: mu
+        // is constant in the attacks)
+        if (l == 0) {
+            adain_in_bwd(0, Ti, [&](int t, int i) __attribute__((always_inline)) { return *lz_fl(gout, t, w, i); },
+                         [&](int, int, f32x4) __attribute__((always_inline)) {});
+            break;
+        }
+        adain_in_bwd(2 * l, Ti, [&](int t, int i) __attribute__((always_inline)) { return *lz_fl(gout, t, w, i); },
+                     [&](int t, int i, f32x4 d) __attribute__((always_inline)) {
+                         st4<PREC>(imgg + (size_t)(LZ_ZR + t) * GRB + (ch0 + 16 * i) * ESZ, d);
+                     });
+        lz_zero_rows<PREC>(imgg, 0, LZ_ZR);
+        lz_zero_rows<PREC>(imgg, LZ_ZR + Ti, LZ_ZR);
+        lz_publish();
+        // conv1^T (+ fold) + the residual branch (adjoint of the x2 nearest upsample) -> g(h_l)
+        for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
+            const int n0 = 16 * chk.f0;
+            const int vlo = max(n0 - 16, -P), vhi = min(n0 + 111, Ti + P - 1);
+            const int r0 = LZ_ZR + vlo + P - ks - 1;
+            __syncthreads();
+            lz_stage<PREC>(WB, imgg, r0, vhi - vlo + ks + 2);
+            __syncthreads();
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
+                rb[f] = LZ_ZR + v + P - r0;
+            }
+            f32x4 acc[2][NF];
+            zero_acc(acc);
+            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), chk.last ? op_c2T(l - 1, 0) : op_c1T(l),
+                                           WB, rb);
+            lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int F = chk.f0 + f - 1, t = 16 * F + c;
+                if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
+                if (t < Ti)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const f32x4 res = up == 2 ? *lz_fl(gin, 2 * t, w, i) + *lz_fl(gin, 2 * t + 1, w, i)
+                                                  : *lz_fl(gin, t, w, i);
+                        *lz_fl(gout, t, w, i) = res + acc[i][f];
+                    }
+            }
+        }
+        cur ^= 1;
+    }
+}
+
 // LDS bytes of the long kernels (the host sets the same)
 constexpr int LZ_LDS_BYTES = 160 * 1024;
 
 #define AVC_LZ_INST(P)                                                    \
     template __global__ void lz_se_fwd<P>(FusedArgs, LongArgs);          \
-    template __global__ void lz_se_bwd<P>(FusedArgs, LongArgs);
+    template __global__ void lz_se_bwd<P>(FusedArgs, LongArgs);          \
+    template __global__ void lz_dec_fwd<P>(DecArgs, LongArgs);           \
+    template __global__ void lz_dec_bwd<P>(DecArgs, LongArgs);
 AVC_LZ_INST(PREC_F32)
 AVC_LZ_INST(PREC_BF16)
 #undef AVC_LZ_INST

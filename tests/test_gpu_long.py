@@ -16,7 +16,8 @@ import torch
 
 import attack_utils
 import avc_native
-from helpers import TOL_GRAD_REL, TOL_SE_REL, cfg_of, check_adv, model_from_fixture, rel
+from helpers import (TOL_GRAD_REL, TOL_GRAD_REL_VC, TOL_SE_REL, TOL_VC_GRAD_L2_MAX, TOL_VC_GRAD_L2_MEDIAN, cfg_of,
+                     check_adv, model_from_fixture, rel)
 from oracle import adain_vc as oracle
 
 pytestmark = pytest.mark.gpu
@@ -144,3 +145,64 @@ def test_long_deterministic_and_shard_invariant(full):
         lo, _, _ = ctx.emb_attack(vc[:4], at[:4], p0[:4], 0.1, 6, precision=prec)
         hi, _, _ = ctx.emb_attack(vc[4:], at[4:], p0[4:], 0.1, 6, precision=prec)
         assert torch.equal(torch.cat([lo, hi]), a)
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_long_vc_golden_T300(full, golden, kind):
+    """e2e / fb attacks made by the reference at vc_src 280, vc_tgt 300, adv_tgt 260 frames:
+    the ContentEncoder (280 frames), the Decoder (35 -> 280 frames), the fb SpeakerEncoder
+    over the decoder output and the attacked SpeakerEncoder (300) all on the long engine."""
+    zl = golden("full_T300")
+    z, m, ctx, _ = full
+    fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
+    adv, info = fn(m, _dev(zl["vc_src"]), _dev(zl["vc_tgt"]), _dev(zl["adv_tgt"]), 0.1, 10,
+                   ptb0=_dev(zl[f"{kind}_ptb0"]), return_info=True)
+    check_adv(adv.detach().cpu().numpy(), zl[f"{kind}_adv_n10"], 10)
+    assert rel(info["grad0"].cpu().numpy(), zl[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
+    np.testing.assert_allclose(info["losses"].cpu().numpy().T, zl[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
+
+
+def test_long_inference_golden_T300(full, golden):
+    zl = golden("full_T300")
+    z, m, ctx, _ = full
+    out = m.inference(_dev(zl["vc_src"]), _dev(zl["vc_tgt"])).cpu().numpy()
+    assert out.shape == zl["inference"].shape
+    assert rel(out, zl["inference"]) <= 1e-4, rel(out, zl["inference"])
+
+
+@pytest.mark.parametrize("Ts", [129, 200, 600])
+def test_long_vc_vs_oracle(full, Ts):
+    """Long ContentEncoder / Decoder lengths vs the float64 oracle: inference and the e2e / fb
+    iteration-0 gradients per utterance (normwise, helpers.TOL_VC_GRAD_*)."""
+    z, m, ctx, w64 = full
+    g = torch.Generator().manual_seed(600 + Ts)
+    src = torch.randn(2, 80, Ts, generator=g)
+    vc, at, p0 = (torch.randn(2, 80, 160, generator=g) for _ in range(3))
+    out = m.inference(src.to(DEV), vc.to(DEV)).cpu().numpy()
+    ref = oracle.inference(w64, cfg_of(z), src.double().numpy(), vc.double().numpy())
+    assert out.shape == ref.shape == (2, 80, 8 * ((Ts + 7) // 8))
+    assert rel(out, ref) <= 1e-4, rel(out, ref)
+    for kind in ("e2e", "fb"):
+        rec = {}
+        getattr(oracle, f"{kind}_attack")(w64, cfg_of(z), src.double().numpy(), vc.double().numpy(),
+                                          at.double().numpy(), 0.1, 1, p0.double().numpy(), record=rec)
+        fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
+        _, info = fn(m, src.to(DEV), vc.to(DEV), at.to(DEV), 0.1, 1, ptb0=p0.to(DEV), return_info=True)
+        gg = info["grad0"].cpu().numpy().astype(np.float64)
+        e = [float(np.linalg.norm(gg[u] - rec["grad0"][u]) / np.linalg.norm(rec["grad0"][u])) for u in range(2)]
+        assert max(e) <= TOL_VC_GRAD_L2_MAX and float(np.median(e)) <= 5 * TOL_VC_GRAD_L2_MEDIAN, (kind, e)
+
+
+def test_long_vc_forced_equals_fused(full):
+    """T = 128 e2e with every component forced onto the long engine vs the fused engine."""
+    z, m, ctx, _ = full
+    g = torch.Generator().manual_seed(88)
+    src, vc, at, p0 = (torch.randn(2, 80, 128, generator=g).to(DEV) for _ in range(4))
+    a_f, i_f = attack_utils.e2e_attack(m, src, vc, at, 0.1, 3, ptb0=p0, return_info=True)
+    ctx.set_engine("long")
+    try:
+        a_l, i_l = attack_utils.e2e_attack(m, src, vc, at, 0.1, 3, ptb0=p0, return_info=True)
+    finally:
+        ctx.set_engine("auto")
+    assert rel(i_l["grad0"].cpu().numpy(), i_f["grad0"].cpu().numpy()) <= TOL_GRAD_REL_VC
+    check_adv(a_l.detach().cpu().numpy(), a_f.detach().cpu().numpy(), 10)
