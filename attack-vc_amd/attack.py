@@ -5,7 +5,9 @@ Same positional arguments and flags as the reference:
   python attack.py MODEL_DIR VC_TGT ADV_TGT OUTPUT [--vc_src SRC] [--eps 0.1]
                    [--n_iters 1500] [--attack_type {e2e,emb,fb}]
 
-plus `--precision {fp32,bf16}` (default fp32, the reference's arithmetic).  The
+plus `--precision {fp32,bf16}` (default fp32, the reference's arithmetic) and the opt-in
+`--update pgd [--pgd_step S]` (sign-gradient step + eps-clamp, include/avc.h AVC_UPDATE_PGD;
+default `adam`, the reference's update).  The
 wav -> mel front end, the attack loop and the Griffin-Lim back end all run in
 libavc's HIP kernels (data_utils.py / attack_utils.py of this package); the
 output is written as 16-bit PCM WAV like soundfile's default.
@@ -19,7 +21,7 @@ from data_utils import denormalize, file2mel, load_model, mel2wav, normalize, wr
 
 
 def main(model_dir: str, vc_src: str, vc_tgt: str, adv_tgt: str, output: str, eps: float, n_iters: int,
-         attack_type: str, precision: str = "fp32"):
+         attack_type: str, precision: str = "fp32", update: str = "adam", pgd_step: float = 1e-3):
     """attack.py:10-75."""
     assert attack_type == "emb" or vc_src is not None
     model, config, attr, device = load_model(model_dir)
@@ -36,12 +38,13 @@ def main(model_dir: str, vc_src: str, vc_tgt: str, adv_tgt: str, output: str, ep
         vc_src = normalize(vc_src, attr)
         vc_src = torch.from_numpy(vc_src).float().T.unsqueeze(0).to(device)
 
+    kw = dict(precision=precision, update=update, pgd_step=pgd_step)
     if attack_type == "e2e":
-        adv_inp = e2e_attack(model, vc_src, vc_tgt, adv_tgt, eps, n_iters, precision=precision)
+        adv_inp = e2e_attack(model, vc_src, vc_tgt, adv_tgt, eps, n_iters, **kw)
     elif attack_type == "emb":
-        adv_inp = emb_attack(model, vc_tgt, adv_tgt, eps, n_iters, precision=precision)
+        adv_inp = emb_attack(model, vc_tgt, adv_tgt, eps, n_iters, **kw)
     elif attack_type == "fb":
-        adv_inp = fb_attack(model, vc_src, vc_tgt, adv_tgt, eps, n_iters, precision=precision)
+        adv_inp = fb_attack(model, vc_src, vc_tgt, adv_tgt, eps, n_iters, **kw)
     else:
         raise NotImplementedError()
 
@@ -69,6 +72,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="The type of adversarial attack to use (end-to-end, embedding, or feedback attack).")
     p.add_argument("--precision", type=str, choices=["fp32", "bf16"], default="fp32",
                    help="Arithmetic of the attack loop (fp32 = the reference's).")
+    p.add_argument("--update", type=str, choices=["adam", "pgd"], default="adam",
+                   help="Perturbation update: adam (the reference's tanh + Adam) or pgd (opt-in sign-gradient "
+                        "step + eps-clamp).")
+    p.add_argument("--pgd_step", type=float, default=1e-3, help="Step size of the pgd update.")
     return p
 
 

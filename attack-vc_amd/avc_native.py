@@ -45,7 +45,10 @@ class VCCfg(ctypes.Structure):
 class AttackOpts(ctypes.Structure):
     _fields_ = [("precision", ctypes.c_int32), ("reduction", ctypes.c_int32),
                 ("use_graph", ctypes.c_int32), ("losses", ctypes.c_void_p),
-                ("grad0", ctypes.c_void_p)]
+                ("grad0", ctypes.c_void_p), ("update", ctypes.c_int32), ("pgd_step", ctypes.c_float)]
+
+
+UPDATE = {"adam": 0, "pgd": 1}
 
 
 class DspCfg(ctypes.Structure):
@@ -212,17 +215,21 @@ class Context:
         if B is not None and t.shape[0] != B:
             raise RuntimeError(f"{name}: batch {t.shape[0]} != {B}")
 
-    def _opts(self, precision, reduction, use_graph, n_iters, like, want_losses, want_grad0):
+    def _opts(self, precision, reduction, use_graph, n_iters, like, want_losses, want_grad0, update="adam",
+              pgd_step=1e-3):
         B = like.shape[0]
+        if update not in UPDATE:
+            raise RuntimeError(f"update must be one of {sorted(UPDATE)}")
         losses = torch.empty(n_iters, B, device=like.device) if want_losses and n_iters > 0 else None
         grad0 = torch.empty_like(like) if want_grad0 and n_iters > 0 else None
         o = AttackOpts(PREC[precision], REDUCE[reduction], 1 if use_graph else 0,
                        losses.data_ptr() if losses is not None else None,
-                       grad0.data_ptr() if grad0 is not None else None)
+                       grad0.data_ptr() if grad0 is not None else None, UPDATE[update], float(pgd_step))
         return o, losses, grad0
 
     def emb_attack(self, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
-                   reduction="independent", use_graph=True, want_losses=False, want_grad0=False):
+                   reduction="independent", use_graph=True, want_losses=False, want_grad0=False, update="adam",
+                   pgd_step=1e-3):
         """avc_emb_attack; an adv_tgt of another length than vc_tgt is embedded on its own first
         (the reference embeds it separately, attack_utils.py:74-75) -> avc_emb_attack_emb."""
         _require_gpu(vc_tgt, adv_tgt, ptb0)
@@ -234,7 +241,8 @@ class Context:
         if ptb0.shape != vc_tgt.shape:
             raise RuntimeError(f"shape mismatch: vc_tgt {tuple(vc_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
         out = torch.empty_like(vc_tgt)
-        o, losses, grad0 = self._opts(precision, reduction, use_graph, n_iters, vc_tgt, want_losses, want_grad0)
+        o, losses, grad0 = self._opts(precision, reduction, use_graph, n_iters, vc_tgt, want_losses, want_grad0,
+                                      update, pgd_step)
         stream = torch.cuda.current_stream(vc_tgt.device).cuda_stream
         tgt_emb = self.se_forward(adv_tgt) if adv_tgt.shape != vc_tgt.shape else None
         with self._lock:
@@ -290,7 +298,8 @@ class Context:
         return out
 
     def vc_attack(self, kind: str, vc_src, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
-                  reduction="independent", use_graph=True, want_losses=False, want_grad0=False):
+                  reduction="independent", use_graph=True, want_losses=False, want_grad0=False, update="adam",
+                  pgd_step=1e-3):
         """kind "e2e" (avc_e2e_attack) or "fb" (avc_fb_attack).  vc_src, vc_tgt and adv_tgt may have
         different lengths (each is loaded from its own wav by attack.py:49-56): then adv_tgt is
         embedded on its own and the *_attack_emb entry points run."""
@@ -305,7 +314,8 @@ class Context:
             raise RuntimeError(f"shape mismatch: vc_tgt {tuple(vc_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
         Ts = vc_src.shape[2]
         out = torch.empty_like(vc_tgt)
-        o, losses, grad0 = self._opts(precision, reduction, use_graph, n_iters, vc_tgt, want_losses, want_grad0)
+        o, losses, grad0 = self._opts(precision, reduction, use_graph, n_iters, vc_tgt, want_losses, want_grad0,
+                                      update, pgd_step)
         stream = torch.cuda.current_stream(vc_tgt.device).cuda_stream
         same = vc_src.shape == vc_tgt.shape == adv_tgt.shape
         tgt_emb = None if same else self.se_forward(adv_tgt)

@@ -26,7 +26,7 @@ __global__ void se_head(HeadArgs A);
 template <bool BW>
 __global__ void se_head_v(HeadArgs A);
 __global__ void attack_init(const float* vc, const float* ptb0, float* ptb, float* m, float* v, float* adv,
-                            float eps, size_t n);
+                            float eps, size_t n, int pgd);
 template <int PREC, int SH>
 __global__ void se_fwd_fused(FusedArgs A);
 template <int PREC, int SH>
@@ -1728,6 +1728,8 @@ static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_t
     if (o.precision != AVC_PREC_FP32 && o.precision != AVC_PREC_BF16) return fail("bad precision %d", o.precision);
     if (o.reduction != AVC_REDUCE_INDEPENDENT && o.reduction != AVC_REDUCE_MEAN)
         return fail("bad reduction %d", o.reduction);
+    if (o.update != AVC_UPDATE_ADAM && !(o.update == AVC_UPDATE_PGD && o.pgd_step > 0.f))
+        return fail("bad update %d (PGD needs pgd_step > 0)", o.update);
     hipStream_t us = (hipStream_t)stream;
     if (ensure_ws(ctx, B, T, n_iters)) return 1;
     Workspace& ws = ctx->ws;
@@ -1749,7 +1751,7 @@ static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_t
     const size_t X = (size_t)B * c.c_in * T;
     const float gscale = (float)(2.0 / (o.reduction == AVC_REDUCE_MEAN ? (double)B * c.c_out : (double)c.c_out));
 
-    const float scal[4] = {eps, gscale, 0.f, 0.f};
+    const float scal[4] = {eps, gscale, 0.f, o.update == AVC_UPDATE_PGD ? o.pgd_step : 0.f};
     if (stage_call_consts(ctx, n_iters, scal)) return 1;
     HIPCHK(hipMemcpyAsync(ws.vc.p, vc_tgt, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     // org_emb = SE(vc_tgt), tgt_emb = SE(adv_tgt)   (attack_utils.py:73-75)
@@ -1765,7 +1767,7 @@ static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_t
                           hipMemcpyDeviceToDevice, ctx->stream));
     // ptb <- ptb0, Adam state 0, adv = vc + eps*tanh(ptb)
     hipLaunchKernelGGL(attack_init, dim3((unsigned)((X + 255) / 256)), dim3(256), 0, ctx->stream, ws.vc.p, ptb0,
-                       ws.ptb.p, ws.m.p, ws.v.p, ws.adv.p, eps, X);
+                       ws.ptb.p, ws.m.p, ws.v.p, ws.adv.p, eps, X, o.update == AVC_UPDATE_PGD ? 1 : 0);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(ws.step, 0, sizeof(int), ctx->stream));
 

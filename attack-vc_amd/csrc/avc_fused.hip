@@ -907,7 +907,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const float nstep = Ad.table[2 * (step - 1)];
     const float bc2s = Ad.table[2 * (step - 1) + 1];
     const float rbc2s = 1.f / bc2s;
-    const AdamStep S{nstep, bc2s, rbc2s, eps};
+    const AdamStep S{nstep, bc2s, rbc2s, eps, A.scal[3]};
     const size_t base4 = (size_t)b * FZ_CIN * T / 4;
     f32x4* __restrict__ ptb4 = reinterpret_cast<f32x4*>(Ad.ptb) + base4;
     f32x4* __restrict__ m4 = reinterpret_cast<f32x4*>(Ad.m) + base4;

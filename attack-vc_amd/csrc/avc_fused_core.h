@@ -454,11 +454,23 @@ __device__ __forceinline__ float fast_tanh(float x) {
 //   bf16 mode: hardware exp2 / rcp / sqrt and explicit fmas (the tail is VALU-bound)
 struct AdamStep {
     float nstep, bc2s, rbc2s, eps;
+    float pgd;           // > 0: the opt-in sign-gradient update with this step (avc_attack_opts.update)
 };
 template <int PREC>
 __device__ __forceinline__ void adam_elem(const AdamArgs& Ad, const AdamStep& S, float gsum, float x, float& p,
                                           float& mm, float& vv, float& g, float& ad) {
 #pragma clang fp contract(off)
+    if (S.pgd > 0.f) {
+        // PGD: ptb holds the perturbation delta itself (adv = vc + delta); delta <-
+        // clamp(delta - step * sign(d loss / d delta), -eps, eps) -- north_star's "sign-grad +
+        // eps-clamp" update (the reference's header optimiser clamps the same way,
+        // models/header_model.py:65); not the reference's attack update (Adam + tanh)
+        g = gsum;
+        const float sg = gsum > 0.f ? 1.f : (gsum < 0.f ? -1.f : 0.f);
+        p = fminf(fmaxf(p - S.pgd * sg, -S.eps), S.eps);
+        ad = x + p;
+        return;
+    }
     if constexpr (PREC == PREC_F32) {
         const float th = tanhf(p);
         g = (gsum * S.eps) * (1.f - th * th);

@@ -126,6 +126,15 @@ __device__ __forceinline__ void epilogue1(const Problem& P, int m, int b, int t,
         const float nstep = A.table[2 * (step - 1)];
         const float bc2s = A.table[2 * (step - 1) + 1];
         float p = A.ptb[idx];
+        const float pgd = P.scal[3];
+        if (pgd > 0.f) {   // opt-in sign-gradient update (see adam_elem, avc_fused_core.h)
+            const float gs = acc + P.aux0[idx];
+            if (A.grad0 && step == 1) A.grad0[idx] = gs;
+            p = fminf(fmaxf(p - pgd * (gs > 0.f ? 1.f : (gs < 0.f ? -1.f : 0.f)), -eps), eps);
+            A.ptb[idx] = p;
+            A.adv[idx] = A.vc[idx] + p;
+            break;
+        }
         const float th = tanhf(p);
         const float g = ((acc + P.aux0[idx]) * eps) * (1.f - th * th);
         if (A.grad0 && step == 1) A.grad0[idx] = g;
@@ -237,6 +246,19 @@ __device__ __forceinline__ bool epilogue4(const Problem& P, int m, int b, int t,
         f32x4 vv = gload<f32x4>(A.v + idx);
         const f32x4 vc = gload<f32x4>(A.vc + idx);
         f32x4 g, adv;
+        const float pgd = P.scal[3];
+        if (pgd > 0.f) {   // opt-in sign-gradient update (see adam_elem, avc_fused_core.h)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                g[e] = v[e] + gx[e];
+                p[e] = fminf(fmaxf(p[e] - pgd * (g[e] > 0.f ? 1.f : (g[e] < 0.f ? -1.f : 0.f)), -eps), eps);
+                adv[e] = vc[e] + p[e];
+            }
+            if (A.grad0 && step == 1) gstore<f32x4>(A.grad0 + idx, g);
+            gstore<f32x4>(A.ptb + idx, p);
+            gstore<f32x4>(A.adv + idx, adv);
+            return true;
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const float th = tanhf(p[e]);

@@ -74,7 +74,7 @@ struct Problem {
     int32_t both_edges;        // BWD gather: T_out <= pl+pr+1, a column may fold from both ends
     int32_t* tick;             // if set, block (0,0) thread 0 increments it (Adam step counter)
     const int32_t* step;       // Adam step counter (read by EPI_ADAM)
-    const float* scal;         // per-call scalars: [0] = attack eps, [1] = loss-grad scale
+    const float* scal;         // per-call scalars: [0] = attack eps, [1] = loss-grad scale, [3] = PGD step (0: Adam)
     int32_t table_len;         // Adam table entries (step is clamped into [1, table_len])
     int32_t pad2_;
     float* slab;               // split-K partial sums [ksplit][M][N] (fp32), reduced in order
@@ -156,7 +156,7 @@ struct FusedArgs {
     const float* g_pooled;            // bwd input [B][128]
     int32_t* tick;                    // fwd: block 0 advances the Adam step counter
     const int32_t* step;              // bwd: Adam step (1-based)
-    const float* scal;                // [0] = attack eps
+    const float* scal;                // [0] = attack eps, [3] = PGD step (0: Adam)
     int32_t table_len;
     int32_t ce_mode;                  // fwd: ContentEncoder (InstanceNorm before every act after the
                                       // bank, mean_layer output to mu_out instead of the time-mean)

@@ -623,15 +623,17 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
     }
 }
 
+// pgd: the sign-gradient mode keeps delta = eps*tanh(ptb0) itself (the same starting adv)
 __global__ void attack_init(const float* __restrict__ vc, const float* __restrict__ ptb0, float* ptb, float* m,
-                            float* v, float* adv, float eps, size_t n) {
+                            float* v, float* adv, float eps, size_t n, int pgd) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float p = ptb0[i];
-    ptb[i] = p;
+    const float d = eps * tanhf(p);
+    ptb[i] = pgd ? d : p;
     m[i] = 0.f;
     v[i] = 0.f;
-    adv[i] = vc[i] + eps * tanhf(p);
+    adv[i] = vc[i] + d;
 }
 
 template __global__ void se_head_v<false>(HeadArgs);

@@ -762,12 +762,14 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     float* R1 = R0 + FZ_CIN * CH;
     const int nfx = lz_nf(T + 8);
     const AdamArgs& Ad = A.adam;
-    const float eps = A.scal[0];
-    const int step = min(max(*A.step, 1), A.table_len);
-    const float nstep = Ad.table[2 * (step - 1)];
-    const float bc2s = Ad.table[2 * (step - 1) + 1];
+    // gx_out mode (fb: d loss / d x handed on) has no Adam state: its AdamArgs are empty
+    const bool adam = A.gx_out == nullptr;
+    const float eps = adam ? A.scal[0] : 0.f;
+    const int step = adam ? min(max(*A.step, 1), A.table_len) : 1;
+    const float nstep = adam ? Ad.table[2 * (step - 1)] : 0.f;
+    const float bc2s = adam ? Ad.table[2 * (step - 1) + 1] : 1.f;
     const float rbc2s = 1.f / bc2s;
-    const AdamStep S{nstep, bc2s, rbc2s, eps};
+    const AdamStep S{nstep, bc2s, rbc2s, eps, adam ? A.scal[3] : 0.f};
     const size_t xb = (size_t)b * FZ_CIN * T;
     LzChunk chk;
     for (int k = 0; lz_chunk(k, nfx, CHF, chk); ++k) {

@@ -91,12 +91,24 @@ int avc_se_forward(avc_ctx* ctx, const float* x, int B, int T, float* emb, void*
  *                           L = MSE(emb,tgt) - 0.1*MSE(emb,org) (before that step's update)
  *   grad0 (optional)      : [B, c_in, T] device fp32, d L / d ptb at iteration 0
  * Adam(lr=1e-3, betas=(0.9,0.999), eps=1e-8) as torch.optim.Adam defaults. */
+/* Perturbation update.
+ *  ADAM (default): the reference's update -- adv = vc + eps*tanh(ptb), torch.optim.Adam on ptb
+ *                  (attack_utils.py:68-86).
+ *  PGD  (opt-in) : the sign-gradient + eps-clamp update BASELINE.json's north_star describes:
+ *                  adv = vc + delta, delta0 = eps*tanh(ptb0), delta <- clamp(delta - pgd_step *
+ *                  sign(d loss / d delta), -eps, eps).  Not in the reference's attacks (its only
+ *                  eps-clamp is the VSMask header optimiser, models/header_model.py:65): parity
+ *                  of this mode is unpinned; grad0 then holds d loss / d delta. */
+enum { AVC_UPDATE_ADAM = 0, AVC_UPDATE_PGD = 1 };
+
 typedef struct avc_attack_opts {
     int32_t precision;   /* AVC_PREC_* */
     int32_t reduction;   /* AVC_REDUCE_* */
     int32_t use_graph;   /* 1 = replay a captured hipGraph per iteration (default) */
     float* losses;
     float* grad0;
+    int32_t update;      /* AVC_UPDATE_* */
+    float pgd_step;      /* PGD step size (> 0 when update == AVC_UPDATE_PGD) */
 } avc_attack_opts;
 
 int avc_emb_attack(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* ptb0,

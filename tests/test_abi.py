@@ -66,4 +66,4 @@ def test_cpu_tensors_fail_loudly():
 def test_header_struct_layout():
     # SECfg mirrors avc_se_cfg: 9 int32 + subsample[16] + act
     assert ctypes.sizeof(avc_native.SECfg) == 4 * (9 + avc_native.MAX_BLOCKS + 1)
-    assert ctypes.sizeof(avc_native.AttackOpts) == 8 + 8 + 8 + 8
+    assert ctypes.sizeof(avc_native.AttackOpts) == 8 + 8 + 8 + 8 + 8   # ... update, pgd_step

@@ -187,15 +187,11 @@ def test_file2mel_mel2wav_roundtrip(tmp_path):
     assert np.isfinite(w).all()
 
 
-def test_attack_cli_end_to_end(tmp_path, golden):
-    """attack.py main() (the reference's CLI): wav files in, defended wav out, all on the GPU.
-    The three wavs have different lengths, as real utterances do (attack.py:49-56 loads each
-    on its own; the reference's attacks never require equal lengths)."""
+def _model_dir(tmp_path, golden):
     import pickle
 
     import yaml
 
-    import attack
     import helpers
     z = golden("full_T128")
     m = helpers.model_from_fixture(z)
@@ -207,8 +203,19 @@ def test_attack_cli_end_to_end(tmp_path, golden):
     torch.save(m.state_dict(), d / "model.ckpt")
     with open(d / "attr.pkl", "wb") as f:
         pickle.dump({"mean": np.full(80, 0.4), "std": np.full(80, 0.2)}, f)
+    return d, pre
+
+
+@pytest.mark.parametrize("frames", [{"src": 90, "tgt": 110, "adv": 70},        # all within the fused engine
+                                    {"src": 213, "tgt": 266, "adv": 160}])    # 4 s / 5 s / 3 s: long engine
+def test_attack_cli_end_to_end(tmp_path, golden, frames):
+    """attack.py main() (the reference's CLI): wav files in, defended wav out, all on the GPU.
+    The three wavs have different lengths, as real utterances do (attack.py:49-56 loads each
+    on its own; the reference's attacks never require equal lengths); the second case has a
+    5-second vc_tgt (266 frames at hop 300 / 16 kHz)."""
+    import attack
+    d, pre = _model_dir(tmp_path, golden)
     paths = {}
-    frames = {"src": 90, "tgt": 110, "adv": 70}
     for i, k in enumerate(("src", "tgt", "adv")):
         paths[k] = str(tmp_path / f"{k}.wav")
         data_utils.write_wav(paths[k], _signal(300 * frames[k], 16000, 20 + i), 16000)
@@ -219,6 +226,21 @@ def test_attack_cli_end_to_end(tmp_path, golden):
         w, sr = data_utils.read_wav(out)
         # the defended utterance keeps vc_tgt's frames (mel2wav: hop * (T - 1) samples)
         assert sr == 16000 and len(w) == pre["hop_length"] * (n_tgt - 1) and np.isfinite(w).all()
+
+
+def test_inference_cli(tmp_path, golden):
+    """inference.py main() (reference inference.py:9-47): source content in the target's
+    voice; source 4 s (long engine), target 2 s; the output has the source's frames."""
+    import inference
+    d, pre = _model_dir(tmp_path, golden)
+    src, tgt, out = (str(tmp_path / f"{k}.wav") for k in ("src", "tgt", "out"))
+    data_utils.write_wav(src, _signal(300 * 213, 16000, 31), 16000)
+    data_utils.write_wav(tgt, _signal(300 * 107, 16000, 32), 16000)
+    inference.main(str(d), src, tgt, out)
+    n_src = data_utils.file2mel(src, **pre).shape[0]
+    w, sr = data_utils.read_wav(out)
+    assert sr == 16000 and np.isfinite(w).all()
+    assert len(w) == pre["hop_length"] * (8 * ((n_src + 7) // 8) - 1)     # decoder: 8 * ceil(T / 8) frames
 
 
 def test_deemphasis_long_signal():

@@ -217,3 +217,22 @@ def test_multi_gpu_driver_matches_single(gpu, golden):
     one = attack_utils.fb_attack(mf, src, vc, at, 0.1, 4, ptb0=p0).detach()
     two = shard.attack_multi_gpu("fb", [mf, mf], src, vc, at, 0.1, 4, ptb0=p0).detach()
     assert torch.equal(one, two)
+
+
+def test_pgd_update_matches_restatement(gpu, golden):
+    """--update pgd (opt-in, north_star's sign-grad + eps-clamp; parity unpinned against the
+    reference, which has no such attack): the GPU emb attack equals the CPU restatement of the
+    mode (tests/test_oracle_golden.pgd_attack_np) except where a sign flips on a near-zero
+    gradient, stays in the eps ball, and is deterministic."""
+    from test_oracle_golden import pgd_attack_np
+    z = golden("small_T32")
+    m = model_from_fixture(z).to(gpu)
+    args = (_dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 20)
+    a = attack_utils.emb_attack(m, *args, ptb0=_dev(z["emb_ptb0"]), update="pgd", pgd_step=5e-3).detach()
+    b = attack_utils.emb_attack(m, *args, ptb0=_dev(z["emb_ptb0"]), update="pgd", pgd_step=5e-3).detach()
+    assert torch.equal(a, b)
+    a = a.cpu().numpy()
+    assert np.abs(a - z["vc_tgt"]).max() <= 0.1 + 1e-6
+    ref = pgd_attack_np(oracle_weights(m), cfg_of(z), z["vc_tgt"], z["adv_tgt"], 0.1, 20, z["emb_ptb0"], 5e-3)
+    d = np.abs(a - ref)
+    assert np.mean(d <= 1e-5) >= 0.99, np.mean(d <= 1e-5)

@@ -243,3 +243,34 @@ def test_long_mixed_lengths_fixture(golden):
         check_adv(adv, z[f"{kind}_adv_n10"], 10)
         assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= (TOL_GRAD_REL if kind == "emb" else TOL_GRAD_REL_VC)
         np.testing.assert_allclose(rec["losses"], z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
+
+
+def pgd_attack_np(w, cfg, vc_tgt, adv_tgt, eps, n_iters, ptb0, step):
+    """CPU restatement of the opt-in PGD update (include/avc.h AVC_UPDATE_PGD) for the emb
+    attack: delta0 = eps*tanh(ptb0); delta <- clamp(delta - step*sign(dL/d delta), -eps, eps).
+    Not the reference's update (parity unpinned): only the mode's own definition."""
+    se = cfg["SpeakerEncoder"]
+    dt = vc_tgt.dtype.type
+    org, _ = oracle.se_forward(w, se, vc_tgt)
+    tgt, _ = oracle.se_forward(w, se, adv_tgt)
+    d = dt(eps) * np.tanh(ptb0.astype(vc_tgt.dtype))
+    n_el = int(np.prod(org.shape[1:]))
+    for _ in range(n_iters):
+        out, st = oracle.se_forward(w, se, vc_tgt + d)
+        g = oracle.se_backward(w, se, st, oracle.emb_loss_grad(out, tgt, org, n_el))
+        d = np.clip(d - dt(step) * np.sign(g), -eps, eps).astype(vc_tgt.dtype)
+    return vc_tgt + d
+
+
+def test_pgd_restatement_properties(golden):
+    """The PGD restatement stays inside the eps ball and lowers the embedding objective."""
+    z = golden("small_T32")
+    w = oracle_weights(model_from_fixture(z))
+    cfg = cfg_of(z)
+    adv = pgd_attack_np(w, cfg, z["vc_tgt"], z["adv_tgt"], 0.1, 20, z["emb_ptb0"], 5e-3)
+    assert np.abs(adv - z["vc_tgt"]).max() <= 0.1 + 1e-6
+    se = cfg["SpeakerEncoder"]
+    tgt, _ = oracle.se_forward(w, se, z["adv_tgt"])
+    e0, _ = oracle.se_forward(w, se, z["vc_tgt"] + 0.1 * np.tanh(z["emb_ptb0"]))
+    e1, _ = oracle.se_forward(w, se, adv)
+    assert ((e1 - tgt) ** 2).mean() < ((e0 - tgt) ** 2).mean()
