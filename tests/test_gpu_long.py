@@ -176,11 +176,11 @@ def test_long_vc_vs_oracle(full, Ts):
     iteration-0 gradients per utterance (normwise, helpers.TOL_VC_GRAD_*)."""
     z, m, ctx, w64 = full
     g = torch.Generator().manual_seed(600 + Ts)
-    src = torch.randn(2, 80, Ts, generator=g)
-    vc, at, p0 = (torch.randn(2, 80, 160, generator=g) for _ in range(3))
+    src = torch.randn(4, 80, Ts, generator=g)
+    vc, at, p0 = (torch.randn(4, 80, 160, generator=g) for _ in range(3))
     out = m.inference(src.to(DEV), vc.to(DEV)).cpu().numpy()
     ref = oracle.inference(w64, cfg_of(z), src.double().numpy(), vc.double().numpy())
-    assert out.shape == ref.shape == (2, 80, 8 * ((Ts + 7) // 8))
+    assert out.shape == ref.shape == (4, 80, 8 * ((Ts + 7) // 8))
     assert rel(out, ref) <= 1e-4, rel(out, ref)
     for kind in ("e2e", "fb"):
         rec = {}
@@ -189,7 +189,7 @@ def test_long_vc_vs_oracle(full, Ts):
         fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
         _, info = fn(m, src.to(DEV), vc.to(DEV), at.to(DEV), 0.1, 1, ptb0=p0.to(DEV), return_info=True)
         gg = info["grad0"].cpu().numpy().astype(np.float64)
-        e = [float(np.linalg.norm(gg[u] - rec["grad0"][u]) / np.linalg.norm(rec["grad0"][u])) for u in range(2)]
+        e = [float(np.linalg.norm(gg[u] - rec["grad0"][u]) / np.linalg.norm(rec["grad0"][u])) for u in range(4)]
         assert max(e) <= TOL_VC_GRAD_L2_MAX and float(np.median(e)) <= 5 * TOL_VC_GRAD_L2_MEDIAN, (kind, e)
 
 
