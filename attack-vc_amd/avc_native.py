@@ -102,6 +102,12 @@ SIGNATURES = [
                                         ctypes.POINTER(ctypes.c_int)]),
     ("avc_pm_forward", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_vsmask_windows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    ("avc_vsmask_protect", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_vsmask_apply_header", ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_dsp_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(DspCfg), ctypes.POINTER(ctypes.c_void_p)]),
     ("avc_dsp_destroy", None, [ctypes.c_void_p]),
     ("avc_dsp_frames", ctypes.c_int, [ctypes.POINTER(DspCfg), ctypes.c_int]),
@@ -346,6 +352,7 @@ class Context:
     def profile(self) -> Tuple[float, Dict[str, Tuple[int, float, float]]]:
         ms, fl = ctypes.c_double(), ctypes.c_double()
         _check(lib().avc_get_profile(self.h, ctypes.byref(ms), ctypes.byref(fl)))
+        self.prof_flop_per_iter = fl.value      # algorithmic FLOPs of one whole-batch iteration
         stats = {}
         for i in range(lib().avc_profile_kernel_count(self.h)):
             name = ctypes.create_string_buffer(128)
@@ -510,6 +517,62 @@ class PMContext:
                                         ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(stream)))
         return y
 
+    def protect(self, mel: torch.Tensor, header: Optional[torch.Tensor], window_size: int = 100,
+                future_step: int = 10, epsilon1: float = 0.1, epsilon2: float = 0.05,
+                epsilon3: float = 0.08) -> torch.Tensor:
+        """VSMask mel loop (vsmask.py:177-208) on mel [B,1,F,T] -> protected mel [B,1,F,T]."""
+        hdr = _vsm_header(header, mel)
+        _require_gpu(mel, *([hdr] if hdr is not None else []))
+        mel = mel.contiguous()
+        B, _, F, T = mel.shape
+        out = torch.empty_like(mel)
+        stream = torch.cuda.current_stream(mel.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_vsmask_protect(
+                self.h, ctypes.c_void_p(mel.data_ptr()), B, F, T,
+                ctypes.c_void_p(hdr.data_ptr() if hdr is not None else 0), hdr.shape[-1] if hdr is not None else 0,
+                int(window_size), int(future_step), float(epsilon1), float(epsilon2), float(epsilon3),
+                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+        return out
+
+
+def _vsm_header(header: Optional[torch.Tensor], mel: torch.Tensor) -> Optional[torch.Tensor]:
+    """[1,1,F,Th] (header_model.py:22) or [F,Th] header -> contiguous [F,Th] on mel's device."""
+    if mel.dim() != 4 or mel.shape[1] != 1:
+        raise RuntimeError(f"VSMask expects a mel of shape [B, 1, F, T], got {tuple(mel.shape)}")
+    if header is None:
+        return None
+    h = header.detach()
+    if h.dim() == 4 and h.shape[:2] == (1, 1):
+        h = h[0, 0]
+    if h.dim() != 2 or h.shape[0] != mel.shape[2]:
+        raise RuntimeError(f"header of shape {tuple(header.shape)} does not match mel bins {mel.shape[2]}")
+    if h.device != mel.device:
+        raise RuntimeError(f"header on {h.device}, mel on {mel.device}")
+    return h.contiguous()
+
+
+def vsmask_apply_header(mel: torch.Tensor, header: torch.Tensor) -> torch.Tensor:
+    """UniversalPerturbationHeader.apply_header (header_model.py:70-95) on the MI355X."""
+    hdr = _vsm_header(header, mel)
+    _require_gpu(mel, hdr)
+    mel = mel.contiguous()
+    B, _, F, T = mel.shape
+    out = torch.empty_like(mel)
+    dev = mel.device.index if mel.device.index is not None else torch.cuda.current_device()
+    stream = torch.cuda.current_stream(mel.device).cuda_stream
+    _check(lib().avc_vsmask_apply_header(dev, ctypes.c_void_p(mel.data_ptr()), B, F, T,
+                                         ctypes.c_void_p(hdr.data_ptr()), hdr.shape[-1],
+                                         ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+    return out
+
+
+def vsmask_windows(T: int, window_size: int = 100, future_step: int = 10) -> int:
+    """Number of predictor windows of the reference loop, len(range(0, T - W, S))."""
+    n = ctypes.c_int()
+    _check(lib().avc_vsmask_windows(int(T), int(window_size), int(future_step), ctypes.byref(n)))
+    return n.value
+
 
 def pm_flat_weights(model: torch.nn.Module) -> torch.Tensor:
     """Floating tensors of a PredictiveModel state_dict in order (num_batches_tracked excluded)."""
@@ -520,17 +583,23 @@ def pm_flat_weights(model: torch.nn.Module) -> torch.Tensor:
 def predictive_forward(model: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
     """PredictiveModel.forward (models/predictive_model.py:87-110), eval semantics, on the MI355X."""
     _require_gpu(x)
+    return pm_context_for(model, x.device).forward(x)
+
+
+def pm_context_for(model: torch.nn.Module, device: torch.device) -> "PMContext":
+    """The libavc PredictiveModel handle of `model` on `device` (re-uploaded when weights change)."""
+    device = torch.device(device)
     if model.training:
         raise RuntimeError("libavc implements PredictiveModel inference (eval mode: BatchNorm running "
                            "statistics); call model.eval() first")
-    dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
+    dev = device.index if device.index is not None else torch.cuda.current_device()
     version = tuple((t.data_ptr(), t._version) for t in model.state_dict().values())
     per = _ctx_cache.setdefault(model, {})
     hit = per.get(("pm", dev))
     if hit is None or hit[0] != version:
         hit = (version, PMContext(pm_flat_weights(model), dev))
         per[("pm", dev)] = hit
-    return hit[1].forward(x)
+    return hit[1]
 
 
 # --- mel front / back end (data_utils.py:16-197) ------------------------------------

@@ -46,6 +46,8 @@ __global__ void dec_bwd_fused(DecArgs A);
 __global__ void dense_batched(DenseArgs D);
 __global__ void pm_conv(PmConvArgs P);
 __global__ void pm_reduce(PmConvArgs P);
+__global__ void vsm_gather(VsmArgs A);
+__global__ void vsm_combine(VsmArgs A);
 }  // namespace avc
 #include "avc_fused_lds.h"
 

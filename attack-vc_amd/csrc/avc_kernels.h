@@ -277,6 +277,20 @@ struct PmConvArgs {
     float* part;                      //      partial sums to part[slice][B*Cout*Ho*Wo]; pm_reduce finishes
 };
 
+// VSMask protect loop (/root/reference/vsmask.py:177-208): window gather + combine/clamp.
+struct VsmArgs {
+    const float* mel;                 // [B][F][T] log-mel (the 4-D [B,1,F,T] view)
+    const float* header;              // [F][Th] universal perturbation header (nullptr: none)
+    const float* y;                   // [B*nw][Ho][Wo] predictor output per window (nw = 0: none)
+    float* win;                       // gather: [B*nw][F][W] windows
+    float* out;                       // [B][F][T]
+    int B, F, T, Th, W, S, nw, Ho, Wo, rows;   // rows = min(F, Ho): predicted rows that land on the mel
+    int low_end, high_start;          // band edges int(F*0.3), int(F*0.7) (utils/audio.py:97-98)
+    float eps1, eps2, eps3;
+    int mode;                         // 0 = protect (band clamp of the summed perturbation),
+                                      // 1 = header_model.apply_header (clamp the sum to [-1, 1])
+};
+
 // Mel front / back end (avc_dsp.hip; data_utils.py:16-197).  One workgroup per pair of
 // STFT frames: the two real frames are the real and imaginary parts of ONE complex
 // n_fft-point FFT in LDS (radix-2, bit-reversed load, twiddles staged in LDS).

@@ -159,4 +159,55 @@ __global__ void __launch_bounds__(256) pm_reduce(PmConvArgs P) {
     P.y[o] = pm_act(s + P.bias[co], P);
 }
 
+// ---- VSMask protect loop (/root/reference/vsmask.py:177-208) ----------------------------
+// The reference walks start = 0, S, 2S, ... < T - W, feeds mel[..., start:start+W] (always the
+// UNPERTURBED mel) to the predictor and adds its output at frames [start+W, start+W+Wo).  The
+// windows are independent, so they are gathered into one batch (vsm_gather), predicted by one
+// batched PredictiveModel forward, and summed per element in the reference's order by
+// vsm_combine: acc = mel (+ header) (+ window 0) (+ window 1) ...; pert = acc - mel; band clamp
+// (utils/audio.py:77-116); out = mel + pert.  Every element repeats the reference's fp32 adds
+// in the same order, so the combine is bit-exact given the same predictor outputs.
+
+__global__ void __launch_bounds__(256) vsm_gather(VsmArgs A) {
+    const size_t n = (size_t)A.B * A.nw * A.F * A.W;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const int j = (int)(i % A.W);
+        const size_t r = i / A.W;
+        const int f = (int)(r % A.F);
+        const size_t bk = r / A.F;
+        const int k = (int)(bk % A.nw);
+        const size_t b = bk / A.nw;
+        A.win[i] = A.mel[(b * A.F + f) * A.T + (size_t)k * A.S + j];
+    }
+}
+
+__global__ void __launch_bounds__(256) vsm_combine(VsmArgs A) {
+    const size_t n = (size_t)A.B * A.F * A.T;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const int t = (int)(i % A.T);
+        const size_t r = i / A.T;
+        const int f = (int)(r % A.F);
+        const size_t b = r / A.F;
+        const float m = A.mel[i];
+        float acc = m;
+        if (A.header && t < A.Th) acc += A.header[(size_t)f * A.Th + t];
+        if (A.mode == 1) {
+            A.out[i] = fminf(fmaxf(acc, -1.f), 1.f);
+            continue;
+        }
+        if (A.nw > 0 && f < A.rows && t >= A.W) {
+            // windows k with k*S + W <= t < k*S + W + Wo, ascending k (the reference's order)
+            const int u = t - A.W;
+            int klo = u - A.Wo + 1;
+            klo = klo <= 0 ? 0 : (klo + A.S - 1) / A.S;
+            const int khi = min(A.nw - 1, u / A.S);
+            for (int k = klo; k <= khi; ++k)
+                acc += A.y[(((b * A.nw + k) * A.Ho) + f) * (size_t)A.Wo + (u - k * A.S)];
+        }
+        const float e = f < A.low_end ? A.eps1 : (f < A.high_start ? A.eps2 : A.eps3);
+        const float p = fminf(fmaxf(acc - m, -e), e);
+        A.out[i] = m + p;
+    }
+}
+
 }  // namespace avc

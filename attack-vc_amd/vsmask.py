@@ -1,0 +1,123 @@
+"""VSMask mel protection (/root/reference/vsmask.py, models/header_model.py) on MI355X.
+
+Mirrors the reference's classes with the same names, constructor arguments and defaults:
+
+  * ``UniversalPerturbationHeader`` (header_model.py:7-104): the [1, 1, 80, 100] header,
+    ``load``/``save`` and ``apply_header`` (libavc ``avc_vsmask_apply_header``).
+  * ``VSMask`` (vsmask.py:14-213): loads a PredictiveModel state_dict and a header, and
+    ``protect_mel`` runs the sliding-window loop of ``_protect_waveform`` (vsmask.py:177-208)
+    in libavc: window gather -> ONE batched PredictiveModel forward over every window ->
+    per-element combine in the reference's add order -> per-band clamp
+    (``avc_vsmask_protect``).
+
+The mel front / back end of the reference (utils/audio.py's torchaudio MelSpectrogram,
+InverseMelScale and GriffinLim) is outside the accelerated path: protect_mel
+takes and returns the log-mel.  The reference loop as shipped cannot run (3-D mel indexed
+as 4-D; 95 predicted rows added to an 80-row mel); the settlement -- 4-D [B, 1, F, T] mel,
+predicted rows cropped to F -- is documented in include/avc.h and oracle/vsmask.py.
+
+CLI (mel in, mel out; .npy [1, F, T] / [B, 1, F, T] / [F, T]):
+
+  python vsmask.py --predictive_model PM.pt --header HEADER.pt --input mel.npy --output out.npy
+"""
+import argparse
+from typing import Optional
+
+import numpy as np
+import torch
+
+import avc_native
+from predictive_model import PredictiveModel
+
+
+class UniversalPerturbationHeader:
+    """header_model.py:7-104 (optimisation -- train_header.py -- is not part of this path)."""
+
+    def __init__(self, mel_bins: int = 80, time_length: int = 100, device: str = "cuda"):
+        self.mel_bins = mel_bins
+        self.time_length = time_length
+        self.device = device
+        self.header = torch.zeros((1, 1, mel_bins, time_length), device=device)
+        self.header.requires_grad = True
+
+    def optimize(self, *args, **kwargs):
+        raise NotImplementedError("UniversalPerturbationHeader.optimize (header training, header_model.py:25-68) "
+                                  "is outside libavc's accelerated path")
+
+    def apply_header(self, source_mel: torch.Tensor) -> torch.Tensor:
+        """header_model.py:70-95: mel [B,1,F,T] + header on frames [0, min(T, 100)), clamped to [-1, 1]."""
+        return avc_native.vsmask_apply_header(source_mel, self.header)
+
+    def save(self, path: str) -> None:
+        torch.save(self.header.detach(), path)
+
+    def load(self, path: str) -> None:
+        h = torch.load(path, map_location=self.device, weights_only=True)
+        if not isinstance(h, torch.Tensor) or h.dim() != 4 or h.shape[:2] != (1, 1):
+            raise RuntimeError(f"{path}: expected a [1, 1, F, T] header tensor")
+        self.header = h.float()
+        self.mel_bins, self.time_length = int(h.shape[2]), int(h.shape[3])
+        self.header.requires_grad = True
+
+
+class VSMask:
+    """vsmask.py:14-39 constructor; protect_mel = the mel loop of _protect_waveform."""
+
+    def __init__(self, predictive_model_path: Optional[str], header_path: Optional[str],
+                 device: str = "cuda"):
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("libavc runs VSMask on MI355X (ROCm) devices only")
+        self.predictive_model = PredictiveModel().to(self.device)
+        if predictive_model_path is not None:
+            sd = torch.load(predictive_model_path, map_location=self.device, weights_only=True)
+            self.predictive_model.load_state_dict(sd)
+        self.predictive_model.eval()
+        self.header = UniversalPerturbationHeader(device=self.device)
+        if header_path is not None:
+            self.header.load(header_path)
+
+    def protect_mel(self, mel_spec: torch.Tensor, window_size: int = 100, future_step: int = 10,
+                    epsilon1: float = 0.1, epsilon2: float = 0.05, epsilon3: float = 0.08) -> torch.Tensor:
+        """vsmask.py:181-208 on a log-mel [B,1,F,T] (or [1,F,T] / [F,T]); returns the same shape."""
+        shape = mel_spec.shape
+        if mel_spec.dim() == 2:
+            mel4 = mel_spec[None, None]
+        elif mel_spec.dim() == 3:
+            mel4 = mel_spec.unsqueeze(1)          # [B, F, T] -> [B, 1, F, T] (SURVEY 2 note A)
+        else:
+            mel4 = mel_spec
+        ctx = avc_native.pm_context_for(self.predictive_model, mel4.device)
+        out = ctx.protect(mel4.float(), self.header.header, window_size, future_step,
+                          epsilon1, epsilon2, epsilon3)
+        return out.reshape(shape)
+
+    def protect_file(self, *args, **kwargs):
+        raise NotImplementedError("protect_file needs the torchaudio mel front/back end (utils/audio.py), "
+                                  "which is outside libavc's accelerated path; use protect_mel")
+
+    protect_stream = protect_file
+
+
+def main(argv=None):
+    """vsmask.py:215-264 argument names, with mel .npy files in place of audio."""
+    p = argparse.ArgumentParser(description="VSMask mel protection on MI355X")
+    p.add_argument("--predictive_model", type=str, required=True)
+    p.add_argument("--header", type=str, required=True)
+    p.add_argument("--input", type=str, required=True, help="log-mel .npy ([F,T], [1,F,T] or [B,1,F,T])")
+    p.add_argument("--output", type=str, required=True)
+    p.add_argument("--window_size", type=int, default=100)
+    p.add_argument("--future_step", type=int, default=10)
+    p.add_argument("--epsilon1", type=float, default=0.1)
+    p.add_argument("--epsilon2", type=float, default=0.05)
+    p.add_argument("--epsilon3", type=float, default=0.08)
+    p.add_argument("--device", type=str, default="cuda")
+    a = p.parse_args(argv)
+    vs = VSMask(a.predictive_model, a.header, device=a.device)
+    mel = torch.from_numpy(np.load(a.input).astype(np.float32)).to(vs.device)
+    out = vs.protect_mel(mel, a.window_size, a.future_step, a.epsilon1, a.epsilon2, a.epsilon3)
+    np.save(a.output, out.cpu().numpy())
+
+
+if __name__ == "__main__":
+    main()

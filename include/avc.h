@@ -16,6 +16,8 @@
  *   avc_inference    replaces  AdaInVC.inference         (/root/reference/models.py:472-489)
  *   avc_attach_vc    replaces  load_state_dict of content_encoder / decoder (models.py:121-208, 346-435)
  *   avc_pm_forward   replaces  PredictiveModel.forward   (/root/reference/models/predictive_model.py:87-110)
+ *   avc_vsmask_protect replaces VSMask._protect_waveform's mel loop (/root/reference/vsmask.py:177-208)
+ *   avc_vsmask_apply_header replaces UniversalPerturbationHeader.apply_header (models/header_model.py:70-95)
  *   avc_dsp_wav2mel  replaces  data_utils.file2mel after load/trim (+ normalize) (/root/reference/data_utils.py:65-118, 35-47)
  *   avc_dsp_mel2wav  replaces  data_utils.mel2wav (+ denormalize)   (/root/reference/data_utils.py:121-165, 50-62)
  *   avc_dsp_griffin_lim replaces data_utils.griffin_lim            (/root/reference/data_utils.py:168-197)
@@ -192,6 +194,29 @@ void avc_pm_destroy(avc_pm* pm);
 int avc_pm_out_shape(int H, int W, int* Ho, int* Wo);
 /* y[B,1,Ho,Wo] = PredictiveModel(x[B,1,H,W]); device pointers, enqueued on `stream` */
 int avc_pm_forward(avc_pm* pm, const float* x, int B, int H, int W, float* y, void* stream);
+
+/* ---- VSMask protect loop (/root/reference/vsmask.py:160-213, utils/audio.py:77-116,
+ * models/header_model.py:70-95) ----
+ * avc_vsmask_protect replaces VSMask._protect_waveform between waveform_to_mel and
+ * mel_to_waveform (vsmask.py:181-208):
+ *   acc = mel; acc[..., :min(T, Th)] += header;
+ *   for start in range(0, T - W, S): acc[..., start+W : start+W+Wo] += PM(mel[..., start:start+W]);
+ *   out = mel + band_clamp(acc - mel)   (f < int(F*0.3): eps1; f < int(F*0.7): eps2; else eps3)
+ * mel [B][F][T] (the 4-D [B,1,F,T] mel the loop indexes); header [F][Th] or NULL; out
+ * [B][F][T], must not alias mel; all device pointers, enqueued on `stream`.  The reference
+ * as shipped cannot run this loop (SURVEY.md 2 note A): its mel is 3-D and its predictor
+ * emits 95 rows for an 80-row mel.  Settled as: 4-D mel, predictor rows [0, min(F, Ho))
+ * added, rows beyond F dropped.  All windows predict from the UNPERTURBED mel (as the
+ * reference), so they run as one batched PredictiveModel forward.  The handle's scratch
+ * is reused by every call: use one stream per avc_pm handle. */
+int avc_vsmask_windows(int T, int window_size, int future_step, int* n_windows);
+int avc_vsmask_protect(avc_pm* pm, const float* mel, int B, int F, int T, const float* header, int Th,
+                       int window_size, int future_step, float eps1, float eps2, float eps3, float* out,
+                       void* stream);
+/* UniversalPerturbationHeader.apply_header (header_model.py:70-95):
+ * out = clamp(mel + header on frames [0, min(T, Th)), -1, 1). */
+int avc_vsmask_apply_header(int device, const float* mel, int B, int F, int T, const float* header, int Th,
+                            float* out, void* stream);
 
 /* ---- Mel front / back end (data_utils.py:16-197) ----
  * The reference's preprocess section of config.yaml.  librosa (<= 0.9, the version the
