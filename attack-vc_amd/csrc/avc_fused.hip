@@ -348,7 +348,11 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     f32x4 b_in[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) b_in[i] = *reinterpret_cast<const f32x4*>(A.w.b_in + ch0 + 16 * i);
-    for (int kb = 0; kb < nb; ++kb) {
+    // one bank kernel + its in_conv block; compile-time kb for the standard shape (every
+    // GEMM's step count and operand map a constant: the runtime loop's K loops carried ~4x
+    // the VALU/SALU work per step)
+    auto bank_fwd = [&](auto KB) __attribute__((always_inline)) {
+        const int kb = KB;
         const int k = kb + 1;
         const int pl = k / 2;
         f32x4 bkb[2];
@@ -372,7 +376,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = act_f(acc[i][f][r] + bi[r], act);
-                    mk.put(i, f, r, y[r] > 0.f);
+                    mk.put(i, f, r, y[r]);
                 }
                 const int t = 16 * f + c;
                 if (t < T) st4<PREC>(BK + t * RS + (ch0 + 16 * i) * ESZ, y);
@@ -387,6 +391,11 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc_h, nf0, ring, op_inb(kb), kb + 1 < nb ? op_bank(kb + 1) : op_inx(), BK, rb);
         if (!DBUF) __syncthreads();
         FZ_PH();
+    };
+    if constexpr (STD != 0) {
+        static_for<0, StdSE::NB>([&](auto KB) __attribute__((always_inline)) { bank_fwd(KB); });
+    } else {
+        for (int kb = 0; kb < nb; ++kb) bank_fwd(kb);
     }
     {   // in_conv, x block (K = 80)
 #pragma unroll
@@ -417,7 +426,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = act_f(acc_h[i][f][r], act);
-                    mk.put(i, f, r, y[r] > 0.f);
+                    mk.put(i, f, r, y[r]);
                 }
                 hres[i][f] = y;
                 const int t = 16 * f + c;
@@ -463,7 +472,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = act_f(acc[i][f][r], act);
-                    mk.put(i, f, r, y[r] > 0.f);
+                    mk.put(i, f, r, y[r]);
                 }
                 const int t = 16 * f + c;
                 if (t < Ti) put_reflect<PREC>(YB, t, Ti, P, (ch0 + 16 * i) * ESZ, y);
@@ -523,7 +532,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = act_f(acc[i][f][r], act);
-                    mk.put(i, f, r, y[r] > 0.f);
+                    mk.put(i, f, r, y[r]);
                     h[r] = y[r] + hres[i][f][r];
                 }
                 hres[i][f] = h;
@@ -682,7 +691,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     f32x4 v;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        v[r] = gh[i][f][r] * mnext.act(i, f, r, act);
+                        v[r] = mnext.gate(i, f, r, gh[i][f][r], act);
                     const int t = 16 * f + c;
                     if (t < To) {
                         st4<PREC>(GB + (ZP + s * t) * RS + (ch0 + 16 * i) * ESZ, v);
@@ -717,7 +726,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     f32x4 v;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        v[r] = acc[i][f][r] * m1.act(i, f, r, act);
+                        v[r] = m1.gate(i, f, r, acc[i][f][r], act);
                     const int t = 16 * f + c;
                     if (t < Ti) st4<PREC>(GB2 + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
                 }
@@ -784,7 +793,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
             if (f >= nf0) continue;
             f32x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = gh[i][f][r] * mnext.act(i, f, r, act);
+            for (int r = 0; r < 4; ++r) v[r] = mnext.gate(i, f, r, gh[i][f][r], act);
             const int t = 16 * f + c;
             if (t < T) st4<PREC>(GP + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
         }
@@ -824,7 +833,8 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         fz_gemm<PREC, 5, NF, FZ_C, 1>(accx, nfx, ring5, opx, op_inTb(0), GP, rb);
     }
     FZ_PH();
-    for (int kb = 0; kb < nb; ++kb) {
+    auto bank_bwd = [&](auto KB) __attribute__((always_inline)) {
+        const int kb = KB;
         const int k = kb + 1, pl = k / 2;
         // g(b_k) for this wave's 32 bank channels = (W_in[:, kb]^T g_pre0) * act'(b_k)
         f32x4 acc[2][8];
@@ -843,7 +853,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 if (f >= nf0) continue;
                 f32x4 v;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] * mb.act(i, f, r, act);
+                for (int r = 0; r < 4; ++r) v[r] = mb.gate(i, f, r, acc[i][f][r], act);
                 const int t = 16 * f + c;
                 if (t < T) st4<PREC>(GBK + (ZPB + t) * RS + (ch0 + 16 * i) * ESZ, v);
             }
@@ -858,6 +868,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         fz_gemm<PREC, 5, NF, FZ_C, -1>(accx, nfx, ring5, op_bankT(kb), kb + 1 < nb ? op_inTb(kb + 1) : op_bankT(kb), GBK, rb);
         __syncthreads();
         FZ_PH();
+    };
+    if constexpr (STD != 0) {
+        static_for<0, StdSE::NB>([&](auto KB) __attribute__((always_inline)) { bank_bwd(KB); });
+    } else {
+        for (int kb = 0; kb < nb; ++kb) bank_bwd(kb);
     }
     fold_edges(accx, T, EB, FSCR);
     FZ_PH();

@@ -399,11 +399,17 @@ __device__ __forceinline__ void inorm_rows(f32x4 (&v)[MT][NF], int nf, int T, f3
 // coalesced 512-B row per (layer, wave); the backward reads its own lane's word back.
 struct MaskAcc {
     unsigned lo = 0, hi = 0;
-    __device__ __forceinline__ void put(int i, int f, int r, bool pos) {
+    // bit = (y > 0) in VALU only: a float is > 0 exactly when its bit pattern is a positive
+    // int, so med3(bits, 0, 1) is the bit (a compare would park one SGPR pair per element:
+    // 64 live lane masks per epilogue spilled through v_writelane / v_readlane)
+    __device__ __forceinline__ void put(int i, int f, int r, float y) {
         if (AVC_FZ_ABLATE & 2) return;
-        const unsigned bit = pos ? (1u << (4 * f + r)) : 0u;
-        if (i == 0) lo |= bit;
-        else hi |= bit;
+        // (inline asm: otherwise LLVM proves the bit equal to the act's own compare and
+        // re-materialises exactly that SGPR-pair compare)
+        unsigned bit;
+        asm("v_med3_i32 %0, %1, 0, 1" : "=v"(bit) : "v"(y));
+        if (i == 0) lo |= bit << (4 * f + r);
+        else hi |= bit << (4 * f + r);
     }
     __device__ __forceinline__ void store(u64* base) const {
         base[threadIdx.x & 63] = ((u64)hi << 32) | lo;
@@ -423,6 +429,16 @@ struct MaskRd {
     __device__ __forceinline__ float act(int i, int f, int r, int actk) const {
         const unsigned w = i == 0 ? lo : hi;
         return ((w >> (4 * f + r)) & 1u) ? 1.f : (actk ? 0.01f : 0.f);
+    }
+    // g * act'(y) of element (i, f, r).  ReLU: the bit sign-extended to a lane mask ANDed
+    // onto g (VALU only; a select would park one SGPR-pair compare per element); the result
+    // differs from g * 0 only in the sign of a zero.  LeakyReLU: g or 0.01 g.
+    __device__ __forceinline__ float gate(int i, int f, int r, float g, int actk) const {
+        const unsigned w = i == 0 ? lo : hi;
+        if (actk) return ((w >> (4 * f + r)) & 1u) ? g : 0.01f * g;
+        int m;
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(w), "s"(4 * f + r));
+        return __builtin_bit_cast(float, __builtin_bit_cast(int, g) & m);
     }
 };
 
