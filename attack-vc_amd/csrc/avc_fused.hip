@@ -114,12 +114,18 @@ __device__ __forceinline__ float head_dot(const HW16& hw, const float* X, int q)
 // Per-row state a thread needs again (biases, targets, the forward activations for the
 // act' masks, E and GB of its own rows) stays in registers; LDS only carries the vectors
 // every thread reads (E, Y_i, GA, GM).
-template <int ND>
+// MODE 1: the emb attack's chain (forward, loss, backward to g_pooled);  MODE 0: forward only
+// (e2e / fb: the embedding for the Decoder), storing the dense activations for MODE 3;
+// MODE 3: backward only, from d loss / d emb (the split-K slices at H.tgt, summed in slice
+// order) with the MODE-0 activations, leaving g_pooled in sm[hpos(c)] (se_head_v modes 1/0/3).
+template <int ND, int MODE = 1>
 __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* sm, float* loss_cur) {
 #pragma clang fp contract(off)
     constexpr int C = FZ_C, D = FZ_C;
     constexpr size_t CC = (size_t)C * C;
     constexpr int NF = 2 * ND + 1, NL = 2 * NF;
+    constexpr int I0 = MODE == 3 ? NF : 0;          // first chain step
+    constexpr int I1 = MODE == 0 ? NF : NL;         // one past the last
     const int act = H.act;
     const int tid = threadIdx.x, q = tid & 3, m0 = tid >> 2, ln = tid & 63, wv = tid >> 6;
     const bool own = q == 0;
@@ -149,24 +155,40 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
                     base + ((size_t)((wv + 4 * h) * 4 + cc) * 64 + ln) * 8));
 #endif
     };
-    float bias[NF][2], tg[2], og[2];
+    float bias[NF][2] = {}, tg[2] = {}, og[2] = {};
+    float e_own[2] = {0.f, 0.f}, gb_own[2] = {0.f, 0.f}, ys[2 * ND][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int m = m0 + 64 * h;
+        if constexpr (MODE != 3) {
 #pragma unroll
-        for (int i = 0; i < NF; ++i) bias[i][h] = H.bias[i * C + m];
-        tg[h] = H.tgt[(size_t)b * D + m];
-        og[h] = H.org[(size_t)b * D + m];
+            for (int i = 0; i < NF; ++i) bias[i][h] = H.bias[i * C + m];
+        }
+        if constexpr (MODE == 1) {
+            tg[h] = H.tgt[(size_t)b * D + m];
+            og[h] = H.org[(size_t)b * D + m];
+        }
+        if constexpr (MODE == 3) {
+#pragma unroll
+            for (int i = 0; i < 2 * ND; ++i) ys[i][h] = H.act_in[((size_t)b * 2 * ND + i) * C + m];
+            if (own) {   // d loss / d emb: the slices summed in order (se_head_v mode 3)
+                const int np = H.tgt_parts > 0 ? H.tgt_parts : 1;
+                float g = 0.f;
+                for (int q2 = 0; q2 < np; ++q2) g += H.tgt[((size_t)q2 * H.B + b) * D + m];
+                GA[hpos(m)] = g;
+            }
+        }
     }
-    const float gscale = H.scal[1];
+    const float gscale = MODE == 1 ? H.scal[1] : 0.f;
     HW16 w0[2], w1[2], w2[2];
-    load_w(w0, IC<0>{});
-    load_w(w1, IC<1>{});
-    load_w(w2, IC<2>{});
+    load_w(w0, IC<I0>{});
+    load_w(w1, IC<I0 + 1>{});
+    load_w(w2, IC<I0 + 2>{});
     __syncthreads();
-    float e_own[2], gb_own[2] = {0.f, 0.f}, ys[2 * ND][2];
+    if constexpr (MODE != 3) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) e_own[h] = E[hpos(m0 + 64 * h)];
+        for (int h = 0; h < 2; ++h) e_own[h] = E[hpos(m0 + 64 * h)];
+    }
 
     auto run_step = [&](auto I, const HW16 (&hw)[2]) __attribute__((always_inline)) {
         constexpr int i = decltype(I)::value;
@@ -183,10 +205,14 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
                 const float y = act_f(o[h] + bias[i][h], act);
                 ys[i][h] = y;
                 if (own) Ys[i * HVS + hpos(m)] = y;
+                if constexpr (MODE == 0)
+                    if (own) H.act_out[((size_t)b * 2 * ND + i) * C + m] = y;
                 if constexpr (i % 2 == 1) {
                     e_own[h] = y + e_own[h];
                     if (own) E[hpos(m)] = e_own[h];
                 }
+            } else if constexpr (i == 2 * ND && MODE == 0) {
+                if (own) H.emb_out[(size_t)b * D + m] = o[h] + bias[2 * ND][h];
             } else if constexpr (i == 2 * ND) {
                 // loss = MSE(emb, tgt) - 0.1 MSE(emb, org) (attack_utils.py:81-82)
                 const float e = o[h] + bias[2 * ND][h];
@@ -207,7 +233,7 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
                     if (own) GM[hpos(m)] = gb_own[h] * act_d(ys[2 * l - 1][h], act);
             }
         }
-        if constexpr (i == 2 * ND) {
+        if constexpr (i == 2 * ND && MODE == 1) {
             __syncthreads();
             if (tid < 64) {   // per-utterance loss, fixed summation order (se_head_v's)
                 float s1 = 0.f, s2 = 0.f;
@@ -226,21 +252,27 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
         }
         __syncthreads();
     };
-    // 3-step register ring: slot i % 3 holds step i and is refilled with step i + 3
-    static_for<0, NL>([&](auto I) __attribute__((always_inline)) {
+    // 3-step register ring: slot (i - I0) % 3 holds step i and is refilled with step i + 3
+    static_for<I0, I1>([&](auto I) __attribute__((always_inline)) {
         constexpr int i = decltype(I)::value;
         auto step = [&](HW16 (&slot)[2]) __attribute__((always_inline)) {
             run_step(I, slot);
-            if constexpr (i + 3 < NL) load_w(slot, IC<i + 3>{});
+            if constexpr (i + 3 < I1) load_w(slot, IC<i + 3>{});
         };
-        if constexpr (i % 3 == 0) step(w0);
-        else if constexpr (i % 3 == 1) step(w1);
+        if constexpr ((i - I0) % 3 == 0) step(w0);
+        else if constexpr ((i - I0) % 3 == 1) step(w1);
         else step(w2);
     });
-    if (own)
+    if constexpr (MODE == 1) {
+        if (own)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) H.g_pooled[(size_t)b * C + m0 + 64 * h] = gb_own[h];
-    if (tid == 0) loss_cur[b] = LS[0];
+            for (int h = 0; h < 2; ++h) H.g_pooled[(size_t)b * C + m0 + 64 * h] = gb_own[h];
+        if (tid == 0) loss_cur[b] = LS[0];
+    } else if constexpr (MODE == 3) {
+        if (own)   // g_pooled for the conv stack's backward, in LDS (E is dead); caller syncs
+#pragma unroll
+            for (int h = 0; h < 2; ++h) E[hpos(m0 + 64 * h)] = gb_own[h];
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -602,7 +634,10 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     FZ_PH();
     if constexpr (PREC == PREC_BF16) {
         if (fh) {
-            if constexpr (STD != 0) se_head_fused<StdSE::NDENSE>(A.head, b, hsm, A.loss_cur);
+            if constexpr (STD != 0) {
+                if (A.fuse_head == 2) se_head_fused<StdSE::NDENSE, 0>(A.head, b, hsm, A.loss_cur);
+                else se_head_fused<StdSE::NDENSE, 1>(A.head, b, hsm, A.loss_cur);
+            }
             FZ_PH();
         }
     }
@@ -644,8 +679,26 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     // LDS clearing so their latency hides under it
     const int TN = STD ? StdSE::Tl(StdSE::NBLK) : A.Tl[A.nblk];
     f32x4 gp[2];
+    if constexpr (PREC == PREC_BF16 && STD != 0) {
+        if (A.fuse_head == 3) {   // e2e / fb: the head's backward (se_head_v mode 3) runs here
+            float* hsm = reinterpret_cast<float*>(fz_lds);
+            se_head_fused<StdSE::NDENSE, 3>(A.head, b, hsm, nullptr);
+            __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 2; ++i) gp[i] = *reinterpret_cast<const f32x4*>(A.g_pooled + (size_t)b * FZ_C + ch0 + 16 * i);
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gp[i][r] = hsm[hpos(ch0 + 16 * i + r)];
+            __syncthreads();
+            FZ_PH();
+        } else {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                gp[i] = *reinterpret_cast<const f32x4*>(A.g_pooled + (size_t)b * FZ_C + ch0 + 16 * i);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) gp[i] = *reinterpret_cast<const f32x4*>(A.g_pooled + (size_t)b * FZ_C + ch0 + 16 * i);
+    }
     const int ns_c = ks * FZ_C / KS;
     const int nblk = STD ? StdSE::NBLK : A.nblk;
     auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
@@ -905,6 +958,10 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     }
     FZ_PH();
 
+    if (A.gx_out && A.losses && tid == 0) {   // fb: the fused head's loss of SE(dec) -> history row
+        const int sn = *A.step;
+        if (sn >= 1 && sn <= A.loss_len) A.losses[(size_t)(sn - 1) * A.B + b] = A.loss_cur[b];
+    }
     if (A.gx_out) {   // d loss / d x handed on (fb: the decoder output's gradient)
         f32x4* gx = reinterpret_cast<f32x4*>(A.gx_out + (size_t)b * FZ_CIN * T);
         const f32x4* R04 = reinterpret_cast<const f32x4*>(R0);

@@ -108,6 +108,8 @@ struct HeadArgs {
     int32_t tgt_parts;        // mode 3: d loss / d emb = sum of this many [B][D] slices at tgt
     const uint16_t* Wr16;     // se_head_v<true> (bf16 mode): Wr / WrT as bf16, 16-byte chunk layout
     const uint16_t* WrT16;
+    float* act_out;           // fused mode 0: [B][2nd][C] the dense activations (for a later mode 3)
+    const float* act_in;      // fused mode 3: the same, written by the mode-0 forward
 };
 
 // ---------------------------------------------------------------------------------
@@ -165,7 +167,9 @@ struct FusedArgs {
     AdamArgs adam;                    // bwd: Adam update + next adv
     FusedW w;
     // emb attack, bf16: the head chain (se_head_v mode 1) runs in the forward's tail
-    int32_t fuse_head;                // fwd: run `head` for this workgroup's utterance
+    int32_t fuse_head;                // fwd: run `head` for this workgroup's utterance in mode 1 (emb
+                                      // loss + backward) or 2 (mode 0: embedding + activations out);
+                                      // bwd: 3 = mode 3 (d loss / d emb -> g_pooled) before the stack
     int32_t loss_len;                 // bwd: rows of `losses`
     float* loss_cur;                  // fwd writes / bwd reads: [B] this iteration's per-utterance loss
     float* losses;                    // bwd: [loss_len][B] loss history (row = step - 1), or null

@@ -526,12 +526,18 @@ def main():
                 "iter_ms_profiled": round(ms_iter, 4),
                 "per_kernel": {k: {"launches_per_iter": v[0] / PROF_ITERS, "avg_ms": round(v[1] / v[0], 4),
                                    "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 2)} for k, v in stats.items()}}
-        tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tpath):
-            key = a.attack + ("_fp32" if a.precision == "fp32" else "")
-            tr = json.load(open(tpath)).get(key, {}).get(name)
-            if tr is not None:
-                roof["traffic"] = tr
+        # HBM bytes and normalised MFMA utilisation of the same kernel from the committed
+        # rocprofv3 PMC passes (scripts/pmc_fused.sh -> scripts/fz_summary.py -> profiles/pmc.json):
+        # PMC counters cannot be read inside this process
+        ppath = os.path.join(ROOT, "profiles", "pmc.json")
+        key = a.attack + ("_fp32" if a.precision == "fp32" else "") + ("" if T == 128 else f"_T{T}")
+        if os.path.exists(ppath):
+            rec = json.load(open(ppath)).get(key, {}).get(name)
+            if rec is not None:
+                roof["traffic"] = rec["traffic"]
+                roof["mfma_util"] = rec["mfma_util"]
+                roof["pmc_source"] = rec["source"]
+                roof["pmc_median_us"] = rec["median_us"]
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -30,6 +30,17 @@ def short(name):
     return n
 
 
+def libname(k):
+    """rocprof kernel name -> the name libavc's HIP-event profile reports (bench.py keys)."""
+    if "<" not in k:
+        return k
+    base, args = k.split("<", 1)
+    first = args.rstrip(">").split(",")[0].strip()
+    if first in ("0", "1") and base not in ("se_head_v",):
+        return f"{base}<{'bf16' if first == '1' else 'fp32'}>"
+    return k
+
+
 def load_counters(d, warm):
     per = defaultdict(lambda: defaultdict(list))     # kernel -> counter -> [values per dispatch]
     for f in sorted(glob.glob(os.path.join(d, "pmc_*", "**", "*counter_collection.csv"), recursive=True)):
@@ -65,6 +76,9 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--out", default=None, help="prefix for <out>_summary.md / _counters.json / _kernel_stats.csv")
     ap.add_argument("--warm", type=int, default=2)
+    ap.add_argument("--pmc-json", default=None, help="merge per-kernel traffic / mfma_util into this file "
+                                                      "under --key (read by bench.py)")
+    ap.add_argument("--key", default=None, help="e.g. emb, emb_fp32, e2e, fb")
     a = ap.parse_args()
     per = load_counters(a.dir, a.warm)
     dur = load_trace(a.dir, a.warm)
@@ -114,6 +128,11 @@ def main():
         st = glob.glob(os.path.join(a.dir, "trace", "**", "*kernel_stats.csv"), recursive=True)
         if st:
             shutil.copy(st[0], a.out + "_kernel_stats.csv")
+    if a.pmc_json and a.key:
+        db = json.load(open(a.pmc_json)) if os.path.exists(a.pmc_json) else {}
+        db[a.key] = {libname(k): {"traffic": d["hbm_bytes"], "mfma_util": d["mfma_util"], "median_us": d["median_us"],
+                                  "source": (a.out or a.dir) + "_summary.md"} for k, d in rows}
+        json.dump(db, open(a.pmc_json, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
