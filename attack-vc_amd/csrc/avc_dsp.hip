@@ -5,7 +5,7 @@
 //   dsp_gl_frames  one Griffin-Lim projection (168-197) per frame pair: STFT of the
 //                  current signal, X = S * est / max(1e-8, |est|), inverse FFT x window
 //   dsp_ola        librosa.istft's overlap-add / window-sum-square / center trim
-//   dsp_deemph     lfilter([1], [1, -preemph]) (161) as a chunked affine scan
+//   dsp_deemph     lfilter([1], [1, -preemph]) (161) as a one-pass tiled affine scan
 // STFT frames are the bandwidth unit: every frame kernel is one workgroup per PAIR of
 // real frames, packed as the real / imaginary parts of one complex N-point FFT
 // (radix-4 DIT passes, bit-reversed load into LDS, twiddles staged in LDS) and separated with
@@ -21,10 +21,8 @@ namespace avc {
 namespace {
 constexpr int DSP_THREADS = 256;
 
-// LDS slot of complex element i: one float2 of padding per 32 (bit-reversed stores and the
-// early radix-4 passes would otherwise hit one bank set 64- / 8-way)
-__device__ __forceinline__ int zp(int i) { return i + (i >> 5); }
-__host__ __device__ constexpr int zlen(int N) { return N + N / 32; }
+__device__ __forceinline__ int zp(int i) { return dsp_zp(i); }
+constexpr int zlen(int N) { return dsp_zlen(N); }
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -278,43 +276,67 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_ola(DspArgs A) {
     A.y[(size_t)b * A.Ly + j] = wss > 1.17549435e-38f ? acc / wss : acc;
 }
 
-// grid (B), 1024 threads: wav = lfilter([1], [1, -a], y) -- chunk recurrences from zero,
-// an inclusive scan of the chunk maps c -> E + a^len c, then the chunks again from their
-// carries
+// grid (B), 1024 threads: wav = lfilter([1], [1, -a], y) in ONE pass over HBM.  Tiles of
+// 1024 x DE samples are staged through LDS with coalesced loads; thread t runs the
+// recurrence over its DE consecutive samples from zero (affine map c -> e + a^DE c), an
+// inclusive scan composes the maps across threads (fixed order: deterministic), the tile's
+// carry enters from the previous tile, and the finished samples leave with coalesced stores.
+constexpr int DE = 8;
 __global__ void __launch_bounds__(1024) dsp_deemph(DspArgs A) {
+    __shared__ float Ts[1024 * DE + 1024 * DE / 32];   // tile, one pad float per 32 (stride-DE reads)
     __shared__ float Ps[1024], Es[1024];
     const int b = blockIdx.x, tid = threadIdx.x, Ly = A.Ly;
     const float a = A.preemph;
     const float* y = A.y + (size_t)b * Ly;
     float* w = A.wav + (size_t)b * Ly;
-    const int C = (Ly + 1023) / 1024;
-    const int lo = min(Ly, tid * C), hi = min(Ly, lo + C);
-    float e = 0.f, p = 1.f;
-    for (int i = lo; i < hi; ++i) {
-        e = fmaf(a, e, y[i]);
-        p *= a;
-    }
-    Ps[tid] = p;
-    Es[tid] = e;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        float pl = 1.f, el = 0.f;
-        if (tid >= off) {
-            pl = Ps[tid - off];
-            el = Es[tid - off];
+    auto tp = [](int i) { return i + (i >> 5); };
+    float aD = 1.f;
+    for (int i = 0; i < DE; ++i) aD *= a;
+    float carry = 0.f;   // wav[tile start - 1]
+    for (int t0 = 0; t0 < Ly; t0 += 1024 * DE) {
+        const int n = min(1024 * DE, Ly - t0);
+#pragma unroll
+        for (int i = 0; i < DE; ++i) {
+            const int k = tid + 1024 * i;
+            Ts[tp(k)] = k < n ? y[t0 + k] : 0.f;
         }
         __syncthreads();
-        if (tid >= off) {
-            // (left then this chunk): c -> E + P (el + pl c)
-            Es[tid] = fmaf(Ps[tid], el, Es[tid]);
-            Ps[tid] = Ps[tid] * pl;
+        float e = 0.f;
+#pragma unroll
+        for (int i = 0; i < DE; ++i) e = fmaf(a, e, Ts[tp(DE * tid + i)]);
+        Ps[tid] = aD;
+        Es[tid] = e;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            float pl = 1.f, el = 0.f;
+            if (tid >= off) {
+                pl = Ps[tid - off];
+                el = Es[tid - off];
+            }
+            __syncthreads();
+            if (tid >= off) {
+                Es[tid] = fmaf(Ps[tid], el, Es[tid]);   // (left then this segment): c -> E + P (el + pl c)
+                Ps[tid] = Ps[tid] * pl;
+            }
+            __syncthreads();
+        }
+        // this segment's incoming value: the scan of the segments before it, fed the tile carry
+        float c = tid == 0 ? carry : fmaf(Ps[tid - 1], carry, Es[tid - 1]);
+        const float next_carry = fmaf(Ps[1023], carry, Es[1023]);
+#pragma unroll
+        for (int i = 0; i < DE; ++i) {
+            const int k = DE * tid + i;
+            c = fmaf(a, c, Ts[tp(k)]);
+            Ts[tp(k)] = c;
         }
         __syncthreads();
-    }
-    float c = tid == 0 ? 0.f : Es[tid - 1];
-    for (int i = lo; i < hi; ++i) {
-        c = fmaf(a, c, y[i]);
-        w[i] = c;
+#pragma unroll
+        for (int i = 0; i < DE; ++i) {
+            const int k = tid + 1024 * i;
+            if (k < n) w[t0 + k] = Ts[tp(k)];
+        }
+        carry = next_carry;
+        __syncthreads();
     }
 }
 

@@ -281,6 +281,14 @@ struct PmConvArgs {
     float* part;                      //      partial sums to part[slice][B*Cout*Ho*Wo]; pm_reduce finishes
 };
 
+// DSP frame kernels (avc_dsp.hip): LDS slot of complex element i of the FFT buffer,
+// i + 2 floor(i/32) + floor(i/64).  Chosen by simulating the ds_read_b64 / ds_write_b64 lane
+// groups of every access pattern at N = 2048 (worst extra-cycle factor per instruction:
+// bit-reversed store 1, radix-4 passes 1 / 2 / 2 / 1 / 1; the former one-per-32 pad had
+// 2 / 1 / 4 / 2 / 1 / 1 -- PMC: 2.85 conflict cycles per LDS instruction in the early passes)
+__host__ __device__ constexpr int dsp_zp(int i) { return i + 2 * (i >> 5) + (i >> 6); }
+__host__ __device__ constexpr int dsp_zlen(int N) { return dsp_zp(N - 1) + 1; }
+
 // VSMask protect loop (/root/reference/vsmask.py:177-208): window gather + combine/clamp.
 struct VsmArgs {
     const float* mel;                 // [B][F][T] log-mel (the 4-D [B,1,F,T] view)
