@@ -76,6 +76,10 @@ SIGNATURES = [
     ("avc_emb_attack_emb", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                           ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_header_optimize", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                           ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_vc_weight_count", ctypes.c_size_t, [ctypes.POINTER(VCCfg)]),
     ("avc_attach_vc", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(VCCfg), ctypes.c_void_p, ctypes.c_size_t]),
     ("avc_vc_out_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -263,6 +267,33 @@ class Context:
                                                 B, T, float(eps), int(n_iters), ctypes.c_void_p(out.data_ptr()),
                                                 ctypes.byref(o), ctypes.c_void_p(stream)))
         return out, losses, grad0
+
+    def header_optimize(self, source, target, header, n_iters: int, epsilon=0.1, lambda_param=0.5, lr=1e-3,
+                        betas=(0.9, 0.999), adam_eps=1e-8, precision="fp32"):
+        """avc_header_optimize (UniversalPerturbationHeader.optimize, header_model.py:25-68):
+        source / target [N, 80, T], header [80, T] -> (new header [80, T], losses [n_iters, N])."""
+        _require_gpu(source, target, header)
+        source, target = source.contiguous(), target.contiguous()
+        c_in = self.cfg["c_in"]
+        self._check_mel("source", source, c_in)
+        N, _, T = source.shape
+        self._check_mel("target", target, c_in, N)
+        if target.shape != source.shape:
+            raise RuntimeError(f"shape mismatch: source {tuple(source.shape)}, target {tuple(target.shape)}")
+        if tuple(header.shape) != (c_in, T):
+            raise RuntimeError(f"header {tuple(header.shape)} does not broadcast onto mels {tuple(source.shape)}")
+        if precision not in PREC:
+            raise RuntimeError(f"precision must be one of {list(PREC)}")
+        hdr = header.detach().clone().contiguous()
+        losses = torch.empty(max(int(n_iters), 1), N, device=source.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream(source.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_header_optimize(self.h, ctypes.c_void_p(source.data_ptr()),
+                                             ctypes.c_void_p(target.data_ptr()), N, T, ctypes.c_void_p(hdr.data_ptr()),
+                                             float(epsilon), float(lambda_param), float(lr), float(betas[0]),
+                                             float(betas[1]), float(adam_eps), int(n_iters), PREC[precision],
+                                             ctypes.c_void_p(losses.data_ptr()), ctypes.c_void_p(stream)))
+        return hdr, losses[:n_iters]
 
     # --- voice-conversion path (ContentEncoder + Decoder) ----------------------------
     def attach_vc(self, ce_cfg: Dict, dec_cfg: Dict, flat: torch.Tensor):

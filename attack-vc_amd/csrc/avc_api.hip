@@ -44,6 +44,8 @@ __global__ void dec_fwd_fused(DecArgs A);
 template <int PREC, int SH>
 __global__ void dec_bwd_fused(DecArgs A);
 __global__ void dense_batched(DenseArgs D);
+__global__ void hdr_compose(HdrArgs A);
+__global__ void hdr_update(HdrArgs A);
 __global__ void pm_conv(PmConvArgs P);
 __global__ void pm_reduce(PmConvArgs P);
 __global__ void vsm_gather(VsmArgs A);
@@ -90,7 +92,8 @@ struct HostConv {
 };
 
 enum LaunchKind {
-    L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD, L_DZ_FWD, L_DZ_BWD, L_DENSE, L_LZ_FWD, L_LZ_BWD, L_LZD_FWD, L_LZD_BWD
+    L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD, L_DZ_FWD, L_DZ_BWD, L_DENSE, L_LZ_FWD, L_LZ_BWD, L_LZD_FWD, L_LZD_BWD,
+    L_HDR_COMPOSE, L_HDR_UPDATE
 };
 constexpr size_t LZ_SHMEM = 160 * 1024;   // the long kernels use the whole LDS (avc_long.hip)
 
@@ -128,6 +131,7 @@ struct Launch {
     int fz_shape = 8;            // L_FZ_*: kernel shape SH (0 = standard config at T = 128, else 1|2|4|8)
     DecArgs dz{};                // L_DZ_*: per-utterance fused Decoder pass (shape: fz_shape 0 | 8)
     DenseArgs dn{};              // L_DENSE: batched conv_affine layer (or its transpose)
+    HdrArgs hd{};                // L_HDR_*: the header optimiser's elementwise ends
     double flop = 0;             // algorithmic FLOPs of this launch
     std::string name;
 };
@@ -154,6 +158,9 @@ struct Workspace {
     int* step = nullptr;
     Plan fwd, iter, iter_bf16;
     hipGraphExec_t graph = nullptr, graph_bf16 = nullptr;
+    Plan hdr_it[2];                   // header optimiser iteration [prec]
+    hipGraphExec_t hdr_graph[2] = {nullptr, nullptr};
+    DevBuf hdr, hdr_m, hdr_v, hdr_gx; // header [F*T], its Adam state, d loss / d x [N][F*T]
     bool built = false;
     int gen = 0;                      // bumped whenever buffers / plans are rebuilt
 };
@@ -685,6 +692,11 @@ static void free_plans(Workspace& ws) {
     if (ws.graph) (void)hipGraphExecDestroy(ws.graph);
     if (ws.graph_bf16) (void)hipGraphExecDestroy(ws.graph_bf16);
     ws.graph = ws.graph_bf16 = nullptr;
+    for (int p = 0; p < 2; ++p) {
+        if (ws.hdr_graph[p]) (void)hipGraphExecDestroy(ws.hdr_graph[p]);
+        ws.hdr_graph[p] = nullptr;
+        free_plan(ws.hdr_it[p]);
+    }
     free_plan(ws.fwd);
     free_plan(ws.iter);
     free_plan(ws.iter_bf16);
@@ -693,7 +705,8 @@ static void free_plans(Workspace& ws) {
 static void free_ws(Workspace& ws) {
     free_plans(ws);
     DevBuf* bufs[] = {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.bank, &ws.h0, &ws.gbank, &ws.gxd,
-                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal, &ws.slab, &ws.pooled, &ws.gpooled, &ws.loss_cur};
+                      &ws.g1, &ws.ghx, &ws.ghy, &ws.gmx, &ws.gmy, &ws.emb_fwd, &ws.org, &ws.tgt, &ws.grad0, &ws.losses, &ws.table, &ws.scal, &ws.slab, &ws.pooled, &ws.gpooled, &ws.loss_cur,
+                      &ws.hdr, &ws.hdr_m, &ws.hdr_v, &ws.hdr_gx};
     for (DevBuf* b : bufs) dfree(*b);
     for (auto& b : ws.a1) dfree(b);
     for (auto& b : ws.a2) dfree(b);
@@ -1354,7 +1367,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
             rc |= dalloc(ws.slab, (size_t)KSPLIT_MAX * std::max(c.c_h, c.c_in) * B * T);
         }
         HIPCHK(hipMalloc(&ws.step, sizeof(int)));
-        rc |= dalloc(ws.scal, 4);
+        rc |= dalloc(ws.scal, 8);
         if (rc) return 1;
     }
     const int cap = std::max(n_iters, std::max(ws.iters_cap, 1));
@@ -1371,7 +1384,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     }
     if (plan_iteration(ctx, ws, ws.iter, PREC_F32)) return 1;
     // autotune with a valid Adam step (1) and eps/gscale (the kernels clamp anyway)
-    const float scal0[4] = {0.1f, 0.f, 0.f, 0.f};
+    const float scal0[8] = {0.1f, 0.f, 0.f, 0.f, 0.1f, 0.f, 0.f, 0.f};
     HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
     HIPCHK(hipMemset(ws.step, 0, sizeof(int)));
     if (autotune(ctx, ws.fwd) || autotune(ctx, ws.iter)) return 1;
@@ -1475,6 +1488,12 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
     }
     case L_DENSE:
         klaunch(ev, false, dense_batched, L.grid, L.block, 0, s, L.dn);
+        return hipGetLastError();
+    case L_HDR_COMPOSE:
+        klaunch(ev, false, hdr_compose, L.grid, L.block, 0, s, L.hd);
+        return hipGetLastError();
+    case L_HDR_UPDATE:
+        klaunch(ev, false, hdr_update, L.grid, L.block, 0, s, L.hd);
         return hipGetLastError();
     case L_LZ_FWD:
         if (L.prec == PREC_F32) klaunch(ev, false, lz_se_fwd<PREC_F32>, L.grid, L.block, L.shmem, s, L.fz, L.lz);
@@ -1691,28 +1710,31 @@ extern "C" int avc_set_profiling(avc_ctx* ctx, int enable) {
 // Adam scalars per step (computed in double like torch's Python-side math) and the per-call
 // scalars [eps, loss-grad scales...] -> ws.table / ws.scal on ctx->stream, asynchronously
 // through the pinned staging buffer
-static int stage_call_consts(avc_ctx* ctx, int n_iters, const float scal[4]) {
+static int stage_call_consts(avc_ctx* ctx, int n_iters, const float scal[4], double lr = 1e-3, double beta1 = 0.9,
+                             double beta2 = 0.999, float lam = 0.1f) {
     Workspace& ws = ctx->ws;
     const size_t nt = 2 * (size_t)std::max(n_iters, 1);
     HIPCHK(hipEventSynchronize(ctx->ev_stage));   // the previous call's staging copies are done
-    if (ctx->stage_n < nt + 4) {
+    if (ctx->stage_n < nt + 8) {
         if (ctx->stage) (void)hipHostFree(ctx->stage);
         ctx->stage = nullptr;
         ctx->stage_n = 0;
-        HIPCHK(hipHostMalloc((void**)&ctx->stage, (nt + 4) * sizeof(float), hipHostMallocDefault));
-        ctx->stage_n = nt + 4;
+        HIPCHK(hipHostMalloc((void**)&ctx->stage, (nt + 8) * sizeof(float), hipHostMallocDefault));
+        ctx->stage_n = nt + 8;
     }
     float* table = ctx->stage;
     for (size_t i = 0; i < nt; ++i) table[i] = 0.f;
     for (int t = 1; t <= n_iters; ++t) {
-        const double bc1 = 1.0 - std::pow(0.9, t);
-        const double bc2 = 1.0 - std::pow(0.999, t);
-        table[2 * (t - 1)] = (float)(-(1e-3 / bc1));
+        const double bc1 = 1.0 - std::pow(beta1, t);
+        const double bc2 = 1.0 - std::pow(beta2, t);
+        table[2 * (t - 1)] = (float)(-(lr / bc1));
         table[2 * (t - 1) + 1] = (float)std::sqrt(bc2);
     }
     for (int i = 0; i < 4; ++i) table[nt + i] = scal[i];
+    table[nt + 4] = lam;
+    for (int i = 5; i < 8; ++i) table[nt + i] = 0.f;
     HIPCHK(hipMemcpyAsync(ws.table.p, table, nt * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ws.scal.p, table + nt, 4 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ws.scal.p, table + nt, 8 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev_stage, ctx->stream));
     return 0;
 }
@@ -1741,7 +1763,7 @@ static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_t
         // stream: an earlier (asynchronous) call's loop on ctx->stream must be finished first
         HIPCHK(hipStreamSynchronize(ctx->stream));
         if (plan_iteration(ctx, ws, ws.iter_bf16, PREC_BF16)) return 1;
-        const float scal0[4] = {0.1f, 0.f, 0.f, 0.f};
+        const float scal0[8] = {0.1f, 0.f, 0.f, 0.f, 0.1f, 0.f, 0.f, 0.f};
         HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
         HIPCHK(hipMemset(ws.step, 0, sizeof(int)));
         if (autotune(ctx, ws.iter_bf16)) return 1;
@@ -1829,6 +1851,111 @@ extern "C" int avc_emb_attack_emb(avc_ctx* ctx, const float* vc_tgt, const float
                                   void* stream) {
     if (!tgt_emb) return fail("avc_emb_attack_emb: null argument");
     return emb_attack_impl(ctx, vc_tgt, nullptr, tgt_emb, ptb0, B, T, eps, n_iters, out_adv, opts, stream);
+}
+
+static int run_iterations(avc_ctx* ctx, Plan& iter, hipGraphExec_t& graph, int n_iters, bool use_graph);
+
+// UniversalPerturbationHeader.optimize (models/header_model.py:25-68) driven as
+// train_header.py:46,77-80 does (torch Adam on the header): per iteration one captured graph
+// of  hdr_compose -> SpeakerEncoder forward (+ loss, head backward) -> input-gradient pass
+// (gx_out) -> hdr_update.  MSE means over all N x c_out elements (F.mse_loss on the batch).
+static int plan_header(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec, int N, int FT) {
+    Launch C;
+    C.kind = L_HDR_COMPOSE;
+    C.grid = dim3((unsigned)std::min<size_t>(((size_t)N * FT + 255) / 256, 8192));
+    C.block = dim3(256);
+    C.name = "hdr_compose";
+    HdrArgs& H = C.hd;
+    H.src = ws.vc.p;
+    H.hdr = ws.hdr.p;
+    H.m = ws.hdr_m.p;
+    H.v = ws.hdr_v.p;
+    H.x = ws.adv.p;
+    H.gx = ws.hdr_gx.p;
+    H.table = ws.table.p;
+    H.step = ws.step;
+    H.table_len = ws.iters_cap;
+    H.N = N;
+    H.FT = FT;
+    pl.launches.push_back(C);
+    if (plan_fused_forward(ctx, ws, pl, ws.adv.p, true, prec) || plan_fused_backward(ctx, ws, pl, prec)) return 1;
+    Launch& Bk = pl.launches.back();
+    Bk.fz.gx_out = ws.hdr_gx.p;
+    const Launch& F = pl.launches[pl.launches.size() - 2];
+    if ((F.kind == L_FZ_FWD) && F.fz.fuse_head) {   // the fused head's loss row, written by the bwd
+        Bk.fz.loss_cur = ws.loss_cur.p;
+        Bk.fz.losses = ws.losses.p;
+        Bk.fz.loss_len = ws.iters_cap;
+    }
+    Launch U = C;
+    U.kind = L_HDR_UPDATE;
+    U.grid = dim3((unsigned)((FT + 255) / 256));
+    U.name = "hdr_update";
+    pl.launches.push_back(U);
+    return 0;
+}
+
+extern "C" int avc_header_optimize(avc_ctx* ctx, const float* source, const float* target, int N, int T,
+                                   float* header, float epsilon, float lambda_param, float lr, float beta1,
+                                   float beta2, float adam_eps, int n_iters, int precision, float* losses,
+                                   void* stream) {
+    if (!ctx || !source || !target || !header) return fail("avc_header_optimize: null argument");
+    if (n_iters < 0) return fail("n_iters must be >= 0");
+    if (precision != AVC_PREC_FP32 && precision != AVC_PREC_BF16) return fail("bad precision %d", precision);
+    if (!(lr > 0.f) || !(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) || !(adam_eps >= 0.f))
+        return fail("avc_header_optimize: bad Adam hyper-parameters");
+    hipStream_t us = (hipStream_t)stream;
+    if (ensure_ws(ctx, N, T, n_iters)) return 1;
+    Workspace& ws = ctx->ws;
+    if (!ws.fused) return fail("the header optimiser runs on the fused / long engine (not LAYERED)");
+    const avc_se_cfg& c = ctx->cfg;
+    const int FT = c.c_in * T;
+    const size_t X = (size_t)N * FT;
+    int rc = dalloc(ws.hdr, FT) | dalloc(ws.hdr_m, FT) | dalloc(ws.hdr_v, FT) | dalloc(ws.hdr_gx, X);
+    if (rc) return 1;
+    const int p = precision == AVC_PREC_BF16 ? 1 : 0;
+    Plan& pl = ws.hdr_it[p];
+    if (pl.launches.empty()) {
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        if (plan_header(ctx, ws, pl, p ? PREC_BF16 : PREC_F32, N, FT)) return 1;
+    }
+    for (Launch& L : pl.launches)
+        if (L.kind == L_HDR_COMPOSE || L.kind == L_HDR_UPDATE) {
+            L.hd.b1c = (float)(1.0 - (double)beta1);
+            L.hd.b2 = beta2;
+            L.hd.b2c = (float)(1.0 - (double)beta2);
+            L.hd.adam_eps = adam_eps;
+            L.hd.clamp_eps = epsilon;
+        }
+    hipGraphExec_t& graph = ws.hdr_graph[p];
+    if (graph) {   // the Adam / clamp constants live in the kernel arguments: re-capture
+        (void)hipGraphExecDestroy(graph);
+        graph = nullptr;
+    }
+    if (begin_call(ctx, us)) return 1;
+    const float gscale = (float)(2.0 / ((double)N * c.c_out));
+    const float scal[4] = {epsilon, gscale, 0.f, 0.f};
+    if (stage_call_consts(ctx, n_iters, scal, lr, beta1, beta2, lambda_param)) return 1;
+    // source_embedding = SE(source), target_embedding = SE(target)   (header_model.py:48-49)
+    HIPCHK(hipMemcpyAsync(ws.vc.p, source, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ws.xin.p, source, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    if (run_plan(ctx, ws.fwd, false)) return 1;
+    HIPCHK(hipMemcpyAsync(ws.org.p, ws.emb_fwd.p, (size_t)N * c.c_out * sizeof(float), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(ws.xin.p, target, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    if (run_plan(ctx, ws.fwd, false)) return 1;
+    HIPCHK(hipMemcpyAsync(ws.tgt.p, ws.emb_fwd.p, (size_t)N * c.c_out * sizeof(float), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(ws.hdr.p, header, FT * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemsetAsync(ws.hdr_m.p, 0, FT * sizeof(float), ctx->stream));
+    HIPCHK(hipMemsetAsync(ws.hdr_v.p, 0, FT * sizeof(float), ctx->stream));
+    HIPCHK(hipMemsetAsync(ws.step, 0, sizeof(int), ctx->stream));
+    if (run_iterations(ctx, pl, graph, n_iters, true)) return 1;
+    HIPCHK(hipMemcpyAsync(header, ws.hdr.p, FT * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    if (losses && n_iters > 0)
+        HIPCHK(hipMemcpyAsync(losses, ws.losses.p, (size_t)n_iters * N * sizeof(float), hipMemcpyDeviceToDevice,
+                              ctx->stream));
+    return end_call(ctx, us);
 }
 
 extern "C" int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_flop_per_iter) {

@@ -180,6 +180,7 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
         }
     }
     const float gscale = MODE == 1 ? H.scal[1] : 0.f;
+    const float lam = MODE == 1 ? H.scal[4] : 0.f;   // weight of the org term (0.1 in the attacks)
     HW16 w0[2], w1[2], w2[2];
     load_w(w0, IC<I0>{});
     load_w(w1, IC<I0 + 1>{});
@@ -218,7 +219,7 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
                 const float e = o[h] + bias[2 * ND][h];
                 const float d1 = e - tg[h], d2 = e - og[h];
                 if (own) {
-                    GA[hpos(m)] = gscale * d1 + gscale * d2 * -0.1f;
+                    GA[hpos(m)] = gscale * d1 + gscale * d2 * -lam;
                     GB[hpos(m)] = d1 * d1;
                     GM[hpos(m)] = d2 * d2;
                 }
@@ -247,7 +248,7 @@ __device__ __forceinline__ void se_head_fused(const HeadArgs& H, int b, float* s
                     s1 += __shfl_xor(s1, off);
                     s2 += __shfl_xor(s2, off);
                 }
-                if (tid == 0) LS[0] = s1 / (float)D - 0.1f * (s2 / (float)D);
+                if (tid == 0) LS[0] = s1 / (float)D - lam * (s2 / (float)D);
             }
         }
         __syncthreads();

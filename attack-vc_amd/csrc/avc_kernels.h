@@ -289,6 +289,22 @@ struct PmConvArgs {
 __host__ __device__ constexpr int dsp_zp(int i) { return i + 2 * (i >> 5) + (i >> 6); }
 __host__ __device__ constexpr int dsp_zlen(int N) { return dsp_zp(N - 1) + 1; }
 
+// UniversalPerturbationHeader.optimize (models/header_model.py:40-65), one iteration's
+// elementwise ends around the SpeakerEncoder forward / input-gradient passes
+struct HdrArgs {
+    const float* src;                 // [N][F*T] source mels (constant)
+    float* hdr;                       // [F*T] the header (in place)
+    float* m;                         // [F*T] Adam state
+    float* v;
+    float* x;                         // compose: [N][F*T] = clamp(src + hdr, -1, 1)
+    const float* gx;                  // update: [N][F*T] d loss / d x
+    const float* table;               // Adam table [iters][2] (-lr / bc1, sqrt(bc2))
+    const int32_t* step;              // 1-based step (advanced by the forward)
+    int32_t table_len, N, FT;
+    float b1c, b2, b2c, adam_eps;     // 1 - beta1, beta2, 1 - beta2, eps
+    float clamp_eps;                  // header clamp (epsilon)
+};
+
 // VSMask protect loop (/root/reference/vsmask.py:177-208): window gather + combine/clamp.
 struct VsmArgs {
     const float* mel;                 // [B][F][T] log-mel (the 4-D [B,1,F,T] view)

@@ -146,6 +146,7 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
     __syncthreads();
 
     const float gscale = A.scal[1];
+    const float lam = A.scal[4];   // weight of the org term (0.1 in the attacks)
     const int step_no = A.mode == 0 ? 0 : *A.step;
 
     auto run_step = [&](int i, const HeadW& w) {
@@ -173,7 +174,7 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
                     const float e = EMB[idx];
                     const float d1 = e - A.tgt[(size_t)b * D + d];
                     const float d2 = e - A.org[(size_t)b * D + d];
-                    g = gscale * d1 + gscale * d2 * -0.1f;
+                    g = gscale * d1 + gscale * d2 * -lam;
                     q1 = d1 * d1;
                     q2 = d2 * d2;
                 }
@@ -197,7 +198,7 @@ __global__ void __launch_bounds__(512) se_head(HeadArgs A) {
                     }
                     const int b = u0 + u;
                     if (lane == 0 && b < A.B)
-                        A.losses[(size_t)(step_no - 1) * A.B + b] = s1 / (float)D - 0.1f * (s2 / (float)D);
+                        A.losses[(size_t)(step_no - 1) * A.B + b] = s1 / (float)D - lam * (s2 / (float)D);
                 }
             }
             __syncthreads();
@@ -489,6 +490,7 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
         if (sink == 1.2345e-31f && tid == 1023) A.g_pooled[0] = sink;   // keeps the loads; never true
     }
     const float gscale = A.scal[1];
+    const float lam = A.scal[4];   // weight of the org term (0.1 in the attacks)
     const int step_no = mode == 0 ? 0 : *A.step;
     __syncthreads();
     // 3-step register ring (8 waves = 2 per SIMD cap a wave at 256 registers; a 4th slot spilled)
@@ -528,7 +530,7 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
                         if (b < Bn) {
                             const float d1 = e[u] - TG[m][u];
                             const float d2 = e[u] - OG[m][u];
-                            gg = gscale * d1 + gscale * d2 * -0.1f;
+                            gg = gscale * d1 + gscale * d2 * -lam;
                             a1 = d1 * d1;
                             a2 = d2 * d2;
                         }
@@ -555,7 +557,7 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
                     s1 += __shfl_xor(s1, o);
                     s2 += __shfl_xor(s2, o);
                 }
-                if (lane == 0) LS[u] = s1 / (float)D - 0.1f * (s2 / (float)D);
+                if (lane == 0) LS[u] = s1 / (float)D - lam * (s2 / (float)D);
             }
         } else if (i == nf) {
             const f32x2 o = dot(hw, K, GA);
@@ -621,6 +623,39 @@ __global__ void __launch_bounds__(512) se_head_v(HeadArgs A) {
         const int b = u0 + u;
         if (b < Bn) A.g_pooled[(size_t)b * C + c] = GB[c][u];
     }
+}
+
+// header_model.py:42-45: perturbed = clamp(source + header, -1, 1) (header broadcast over N)
+__global__ void __launch_bounds__(256) hdr_compose(HdrArgs A) {
+    const size_t n = (size_t)A.N * A.FT;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        A.x[i] = fminf(fmaxf(A.src[i] + A.hdr[i % A.FT], -1.f), 1.f);
+}
+
+// header_model.py:58-65: d loss / d header = sum over the N sources of d loss / d x where the
+// clamp passed it (torch clamp backward: min <= x <= max), summed in source order; torch
+// Adam (_single_tensor_adam: lerp, mul + addcmul, addcdiv) on the header; clamp to
+// [-epsilon, epsilon].  One thread per header element.
+__global__ void __launch_bounds__(256) hdr_update(HdrArgs A) {
+#pragma clang fp contract(off)
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= A.FT) return;
+    const float h = A.hdr[e];
+    float g = 0.f;
+    for (int b = 0; b < A.N; ++b) {
+        const float pre = A.src[(size_t)b * A.FT + e] + h;
+        if (pre >= -1.f && pre <= 1.f) g += A.gx[(size_t)b * A.FT + e];
+    }
+    const int step = min(max(*A.step, 1), A.table_len);
+    const float nstep = A.table[2 * (step - 1)], bc2s = A.table[2 * (step - 1) + 1];
+    float m = A.m[e], v = A.v[e];
+    m = m + A.b1c * (g - m);
+    v = v * A.b2;
+    v = v + A.b2c * g * g;
+    const float p = h + nstep * (m / (sqrtf(v) / bc2s + A.adam_eps));
+    A.m[e] = m;
+    A.v[e] = v;
+    A.hdr[e] = fminf(fmaxf(p, -A.clamp_eps), A.clamp_eps);
 }
 
 // pgd: the sign-gradient mode keeps delta = eps*tanh(ptb0) itself (the same starting adv)

@@ -3,7 +3,8 @@
 Mirrors the reference's classes with the same names, constructor arguments and defaults:
 
   * ``UniversalPerturbationHeader`` (header_model.py:7-104): the [1, 1, 80, 100] header,
-    ``load``/``save`` and ``apply_header`` (libavc ``avc_vsmask_apply_header``).
+    ``optimize`` (libavc ``avc_header_optimize``), ``load``/``save`` and ``apply_header``
+    (libavc ``avc_vsmask_apply_header``).
   * ``VSMask`` (vsmask.py:14-213): loads a PredictiveModel state_dict and a header, and
     ``protect_mel`` runs the sliding-window loop of ``_protect_waveform`` (vsmask.py:177-208)
     in libavc: window gather -> ONE batched PredictiveModel forward over every window ->
@@ -31,7 +32,7 @@ from predictive_model import PredictiveModel
 
 
 class UniversalPerturbationHeader:
-    """header_model.py:7-104 (optimisation -- train_header.py -- is not part of this path)."""
+    """header_model.py:7-104 on libavc."""
 
     def __init__(self, mel_bins: int = 80, time_length: int = 100, device: str = "cuda"):
         self.mel_bins = mel_bins
@@ -40,9 +41,35 @@ class UniversalPerturbationHeader:
         self.header = torch.zeros((1, 1, mel_bins, time_length), device=device)
         self.header.requires_grad = True
 
-    def optimize(self, *args, **kwargs):
-        raise NotImplementedError("UniversalPerturbationHeader.optimize (header training, header_model.py:25-68) "
-                                  "is outside libavc's accelerated path")
+    def optimize(self, source_mel: torch.Tensor, target_mel: torch.Tensor, speaker_encoder, optimizer,
+                 num_iterations: int = 1000, epsilon: float = 0.1, lambda_param: float = 0.5,
+                 precision: str = "fp32") -> None:
+        """header_model.py:25-68 on the MI355X (avc_header_optimize): the whole loop -- clamp
+        (source + header), SpeakerEncoder forward, the loss MSE(., SE(target)) - lambda MSE(.,
+        SE(source)), its input-gradient, torch Adam on the header with `optimizer`'s lr /
+        betas / eps, clamp to +-epsilon -- runs in libavc, one captured graph per iteration.
+
+        source_mel / target_mel: [N, 1, F, T] as train_header.py builds them (or [N, F, T]; the
+        reference's SpeakerEncoder cannot take the 4-D form, SURVEY.md 2 note A).  The header
+        is updated in place; `optimizer`'s own state is not advanced (its hyper-parameters are
+        read from param_groups[0]).  Prints the batch loss every 100 iterations like the
+        reference."""
+        def mel3(x):
+            return x[:, 0] if x.dim() == 4 else x
+        src, tgt = mel3(source_mel).float(), mel3(target_mel).float()
+        g = optimizer.param_groups[0]
+        if g.get("amsgrad") or g.get("weight_decay", 0) or g.get("maximize"):
+            raise RuntimeError("libavc implements plain Adam (no amsgrad / weight_decay / maximize)")
+        ctx = avc_native.context_for(speaker_encoder, src.device)
+        hdr0 = self.header.detach()[0, 0]
+        new, losses = ctx.header_optimize(src, tgt, hdr0, int(num_iterations), epsilon, lambda_param, g["lr"],
+                                          g["betas"], g["eps"], precision)
+        with torch.no_grad():
+            self.header.data.copy_(new.reshape(self.header.shape))
+        batch = losses.mean(dim=1).cpu()
+        for i in range(99, int(num_iterations), 100):
+            print(f"Iteration {i+1}/{num_iterations}, Loss: {batch[i].item():.6f}")
+        self.losses = batch
 
     def apply_header(self, source_mel: torch.Tensor) -> torch.Tensor:
         """header_model.py:70-95: mel [B,1,F,T] + header on frames [0, min(T, 100)), clamped to [-1, 1]."""

@@ -18,6 +18,7 @@
  *   avc_pm_forward   replaces  PredictiveModel.forward   (/root/reference/models/predictive_model.py:87-110)
  *   avc_vsmask_protect replaces VSMask._protect_waveform's mel loop (/root/reference/vsmask.py:177-208)
  *   avc_vsmask_apply_header replaces UniversalPerturbationHeader.apply_header (models/header_model.py:70-95)
+ *   avc_header_optimize replaces UniversalPerturbationHeader.optimize (models/header_model.py:25-68)
  *   avc_dsp_wav2mel  replaces  data_utils.file2mel after load/trim (+ normalize) (/root/reference/data_utils.py:65-118, 35-47)
  *   avc_dsp_mel2wav  replaces  data_utils.mel2wav (+ denormalize)   (/root/reference/data_utils.py:121-165, 50-62)
  *   avc_dsp_griffin_lim replaces data_utils.griffin_lim            (/root/reference/data_utils.py:168-197)
@@ -213,6 +214,20 @@ int avc_vsmask_windows(int T, int window_size, int future_step, int* n_windows);
 int avc_vsmask_protect(avc_pm* pm, const float* mel, int B, int F, int T, const float* header, int Th,
                        int window_size, int future_step, float eps1, float eps2, float eps3, float* out,
                        void* stream);
+/* UniversalPerturbationHeader.optimize (header_model.py:25-68) as train_header.py:46,77-80
+ * drives it (torch Adam(lr, betas, eps) on the header): per iteration
+ *   perturbed = clamp(source + header, -1, 1);
+ *   loss = MSE(SE(perturbed), SE(target)) - lambda_param * MSE(SE(perturbed), SE(source));
+ *   Adam step on the header; header = clamp(header, -epsilon, epsilon).
+ * source / target [N][80][T] (the reference's [N,1,80,T] mels, whose 4-D shape the
+ * SpeakerEncoder cannot take: settled as 3-D); header [80][T] device, in / out (T = the
+ * header length: the reference's broadcast needs equal lengths).  losses [n_iters][N] per-source
+ * loss terms (their mean is the reference's loss) or NULL.  Runs on ctx's SpeakerEncoder with
+ * the fused / long engine; precision AVC_PREC_*. */
+int avc_header_optimize(avc_ctx* ctx, const float* source, const float* target, int N, int T, float* header,
+                        float epsilon, float lambda_param, float lr, float beta1, float beta2, float adam_eps,
+                        int n_iters, int precision, float* losses, void* stream);
+
 /* UniversalPerturbationHeader.apply_header (header_model.py:70-95):
  * out = clamp(mel + header on frames [0, min(T, Th)), -1, 1). */
 int avc_vsmask_apply_header(int device, const float* mel, int B, int F, int T, const float* header, int Th,

@@ -22,6 +22,8 @@ execution of the reference (which fails, and whose torchaudio dependency is abse
 """
 import numpy as np
 
+from oracle import adain_vc as _av
+
 
 def n_windows(T, window_size=100, future_step=10):
     """vsmask.py:186: len(range(0, T - window_size, future_step))."""
@@ -72,3 +74,28 @@ def apply_header(mel, header):
     out[:, :, :, :h.shape[3]] += h.astype(mel.dtype)
     ft = mel.dtype.type
     return np.clip(out, ft(-1.0), ft(1.0))
+
+
+def header_optimize(w, se_cfg, source, target, header, n_iters, epsilon=0.1, lambda_param=0.5, lr=1e-3,
+                    betas=(0.9, 0.999), adam_eps=1e-8):
+    """header_model.py:40-65 (+ train_header.py:46: torch Adam on the header) with the
+    SpeakerEncoder restatement oracle/adain_vc.py.  source / target [N, F, T] (the settled 3-D
+    mels), header [F, T].  Returns (header, per-iteration batch losses)."""
+    dt = source.dtype.type
+    src_emb, _ = _av.se_forward(w, se_cfg, source)
+    tgt_emb, _ = _av.se_forward(w, se_cfg, target)
+    n_el = src_emb.size
+    opt = _av.Adam(header.astype(source.dtype).copy(), lr, betas, adam_eps)
+    losses = []
+    for _ in range(n_iters):
+        pre = source + opt.p
+        x = np.clip(pre, dt(-1), dt(1))
+        emb, st = _av.se_forward(w, se_cfg, x)
+        losses.append(((emb - tgt_emb) ** 2).mean() - lambda_param * ((emb - src_emb) ** 2).mean())
+        norm = dt(2.0 / n_el)
+        g_emb = norm * (emb - tgt_emb) + norm * (emb - src_emb) * dt(-lambda_param)
+        gx = _av.se_backward(w, se_cfg, st, g_emb)
+        g = np.where((pre >= -1) & (pre <= 1), gx, dt(0)).sum(axis=0)
+        opt.step(g)
+        opt.p = np.clip(opt.p, dt(-epsilon), dt(epsilon))
+    return opt.p, np.array(losses)

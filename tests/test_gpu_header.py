@@ -1,0 +1,69 @@
+"""GPU parity of the VSMask header optimiser (libavc avc_header_optimize,
+/root/reference/models/header_model.py:25-68 driven as train_header.py:46,77-80) against the
+restatement oracle/vsmask.py::header_optimize on the float64 SpeakerEncoder oracle.  The
+header loop itself has no reference output to pin (the reference cannot run it as shipped:
+4-D mels into a Conv1d stack, SURVEY.md 2 note A) -- parity unpinned beyond the
+SpeakerEncoder forward / input-gradient, which the golden fixtures pin."""
+import numpy as np
+import pytest
+import torch
+
+import avc_native
+import vsmask
+from helpers import model_from_fixture, oracle_weights, cfg_of
+from oracle import vsmask as vo
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def full(golden):
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    z = golden("full_T128")
+    m = model_from_fixture(z).eval()
+    return m, oracle_weights(m), cfg_of(z)["SpeakerEncoder"]
+
+
+def _mels(N, T, seed):
+    g = np.random.default_rng(seed)
+    return g.uniform(-0.97, 0.97, (N, 80, T)).astype(np.float32), g.uniform(-0.97, 0.97, (N, 80, T)).astype(np.float32)
+
+
+def test_header_optimize_vs_oracle(full):
+    m, w, se = full
+    N, T, n = 4, 100, 8
+    src, tgt = _mels(N, T, 1)
+    hdr0 = (np.random.default_rng(2).uniform(-0.05, 0.05, (80, T))).astype(np.float32)
+    ctx = avc_native.context_for(m.to(DEV).speaker_encoder, DEV)
+    h, losses = ctx.header_optimize(torch.from_numpy(src).to(DEV), torch.from_numpy(tgt).to(DEV),
+                                    torch.from_numpy(hdr0).to(DEV), n, epsilon=0.06, lambda_param=0.5, lr=2e-3)
+    ref, ref_losses = vo.header_optimize(w, se, src.astype(np.float64), tgt.astype(np.float64),
+                                         hdr0.astype(np.float64), n, epsilon=0.06, lambda_param=0.5, lr=2e-3)
+    h = h.cpu().numpy()
+    d = np.abs(h - ref)
+    # Adam normalises every element's step: a gradient element near zero can flip its early
+    # steps between fp32 and float64; the bulk must agree to ~fp32 rounding
+    assert np.abs(h).max() <= 0.06 + 1e-7
+    assert np.mean(d > 1e-5) <= 0.01, np.mean(d > 1e-5)
+    assert d.mean() <= 2e-6, d.mean()
+    np.testing.assert_allclose(losses.mean(dim=1).cpu().numpy(), ref_losses, rtol=1e-4, atol=1e-6)
+
+
+def test_header_optimize_module_bf16_and_shapes(full):
+    m, _, _ = full
+    m = m.to(DEV)
+    N, T = 3, 100
+    src, tgt = _mels(N, T, 3)
+    hdr = vsmask.UniversalPerturbationHeader(device="cuda:0")
+    opt = torch.optim.Adam([hdr.header], lr=1e-3)
+    s4 = torch.from_numpy(src).to(DEV)[:, None]      # [N, 1, 80, T] as train_header.py builds them
+    t4 = torch.from_numpy(tgt).to(DEV)[:, None]
+    hdr.optimize(s4, t4, m.speaker_encoder, opt, num_iterations=200, epsilon=0.1, lambda_param=0.5, precision="bf16")
+    assert hdr.header.shape == (1, 1, 80, T) and hdr.header.requires_grad
+    assert float(hdr.header.detach().abs().max()) <= 0.1 + 1e-7
+    assert hdr.losses[-1] < hdr.losses[0]
+    with pytest.raises(RuntimeError):
+        avc_native.context_for(m.speaker_encoder, DEV).header_optimize(
+            torch.from_numpy(src).to(DEV), torch.from_numpy(tgt).to(DEV), torch.zeros(80, T - 1, device=DEV), 1)

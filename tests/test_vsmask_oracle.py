@@ -86,3 +86,22 @@ def test_float32_loop_equals_reordered_sum(T):
             p = np.float32(min(max(np.float32(a - mel[0, 0, f, t]), -e), e))
             out[f, t] = np.float32(mel[0, 0, f, t] + p)
     assert np.array_equal(out, ref[0, 0])
+
+
+def test_header_optimize_restatement_properties(golden):
+    """The header-optimisation restatement (header_model.py:40-65) keeps the header inside
+    +-epsilon, lowers its objective and matches a hand-computed first Adam step's size."""
+    from helpers import cfg_of, model_from_fixture, oracle_weights
+    z = golden("small_T32")
+    w = oracle_weights(model_from_fixture(z))
+    se = cfg_of(z)["SpeakerEncoder"]
+    rng = np.random.default_rng(5)
+    src = rng.uniform(-0.95, 0.95, (3, 80, 32))
+    tgt = rng.uniform(-0.95, 0.95, (3, 80, 32))
+    hdr, losses = vo.header_optimize(w, se, src, tgt, np.zeros((80, 32)), 25, epsilon=0.05, lr=2e-3)
+    assert np.abs(hdr).max() <= 0.05 + 1e-12
+    assert losses[-1] < losses[0]
+    h1, _ = vo.header_optimize(w, se, src, tgt, np.zeros((80, 32)), 1, epsilon=0.05, lr=2e-3)
+    # Adam's first step is lr * g / (|g| + eps): at most lr, ~lr wherever |g| >> eps
+    moved = np.abs(h1[np.abs(h1) > 0])
+    assert moved.max() <= 2e-3 * (1 + 1e-9) and abs(np.median(moved) - 2e-3) <= 2e-5
