@@ -91,6 +91,84 @@ __device__ __forceinline__ void lz_stage(char* lds, const char* img, int r0, int
     }
 }
 
+// rows [r0, r0 + n) of a global operand image -> LDS rows [0, n) (stride RS) by LDS-DMA
+// (global_load_lds_dwordx4), NOT waited for: every wave issues NI 1-KB pieces of the padded
+// LDS layout (a piece's lanes that fall on a row's pad slots or past row n load a duplicate
+// that is never read).  A compile-time piece count keeps the waitcnt bookkeeping of the
+// K loops that follow exact.  n <= NRMAX.
+template <int PREC, int NRMAX>
+struct LzDma {
+    static constexpr int SPR = Lz<PREC>::RS / 16, PPR = Lz<PREC>::GRB / 16;
+    static constexpr int NI = (NRMAX * SPR + 255) / 256;    // pieces per wave
+    static constexpr int BUFB = NI * 256 * 16;               // LDS bytes a stage buffer spans
+};
+template <int PREC, int NRMAX>
+__device__ __forceinline__ void lz_stage_dma(char* lds, const char* img, int r0, int n) {
+    using D = LzDma<PREC, NRMAX>;
+    constexpr int GRB = Lz<PREC>::GRB;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const char* src = img + (size_t)r0 * GRB;
+#pragma unroll
+    for (int i = 0; i < D::NI; ++i) {
+        const int base = (i * 4 + w) * 64;                   // the piece's first slot (wave-uniform)
+        const int q = base + lane;
+        int r = q / D::SPR, p = q - r * D::SPR;
+        r = r < n ? r : n - 1;
+        p = p < D::PPR ? p : 0;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (size_t)r * GRB + p * 16),
+                                         (__attribute__((address_space(3))) void*)(lds + (size_t)base * 16), 16, 0,
+                                         0);
+    }
+}
+
+// Chunk-input staging of one layer.  bf16 with every window <= NRMAX rows: two LDS buffers;
+// chunk k+1's rows are issued by LDS-DMA right after chunk k's GEMM (issue_next), so the
+// global round trip hides under chunk k's epilogue.  (Issued any earlier, the compiler puts
+// a full vmcnt(0) before the GEMM's first LDS read -- it cannot tell the DMA's LDS target
+// from the buffer being read -- and its weight-ring waits would over-wait on the DMA.)
+// Otherwise the synchronous lz_stage.
+template <int PREC, int NRMAX>
+struct LzPipe {
+    char* b0;
+    int boff;                                                // second buffer at b0 + boff (0: one buffer)
+    bool dma;
+    int nfrag;
+    __device__ __forceinline__ LzPipe(char* WB, int nfrag_, int nr_bound) : nfrag(nfrag_) {
+        dma = PREC == PREC_BF16 && nr_bound <= NRMAX;
+        b0 = WB;
+        boff = dma ? LzDma<PREC, NRMAX>::BUFB : 0;
+    }
+    template <class R0F, class NRF>
+    __device__ __forceinline__ void prime(const char* img, R0F r0f, NRF nrf) {
+        if (!dma) return;
+        LzChunk c0;
+        lz_chunk(0, nfrag, LZ_CHF, c0);
+        __syncthreads();                                     // earlier readers of b0 are done
+        lz_stage_dma<PREC, NRMAX>(b0, img, r0f(c0), nrf(c0));
+    }
+    // the staged rows of chunk k (all waves may read them on return)
+    template <class R0F, class NRF>
+    __device__ __forceinline__ const char* next(int k, const LzChunk& chk, const char* img, R0F r0f, NRF nrf) {
+        if (dma) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();                                 // chunk k landed everywhere; chunk k-1 read
+            // (buffers by offset arithmetic: a select of two pointers became a scratch-indexed load)
+            return b0 + (k & 1) * boff;
+        }
+        __syncthreads();
+        lz_stage<PREC>(b0, img, r0f(chk), nrf(chk));
+        __syncthreads();
+        return b0;
+    }
+    // after chunk k's last LDS read of this pass: chunk k+1's rows into the other buffer
+    template <class R0F, class NRF>
+    __device__ __forceinline__ void issue_next(int k, const char* img, R0F r0f, NRF nrf) {
+        if (!dma) return;
+        LzChunk nx;
+        if (lz_chunk(k + 1, nfrag, LZ_CHF, nx)) lz_stage_dma<PREC, NRMAX>(b0 + ((k + 1) & 1) * boff, img, r0f(nx), nrf(nx));
+    }
+};
+
 // zero image rows [r0, r0 + n) (whole workgroup)
 template <int PREC>
 __device__ __forceinline__ void lz_zero_rows(char* img, int r0, int n) {
@@ -313,7 +391,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             __syncthreads();
             f32x4 acc_h[2][NF];
             zero_acc(acc_h);
-            for (int kb = 0; kb < nb; ++kb) {
+            auto bank_step = [&](auto KB) __attribute__((always_inline)) {
+                const int kb = KB;
                 const int kk = kb + 1, pl = kk / 2;
                 f32x4 bkb[2];
 #pragma unroll
@@ -341,7 +420,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                 const AOp nxt = kb + 1 < nb ? op_bank(kb + 1) : op_inx();
                 fz_gemm<PREC, 2, NF, FZ_C, 1>(acc_h, IC<NF>{}, ring, op_inb(kb), nxt, BK, rb);
                 if (!DBUF) __syncthreads();
-            }
+            };
+            for (int kb = 0; kb < nb; ++kb) bank_step(kb);
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T - 1) - n0 + 4;
             fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc_h, IC<NF>{}, ring, op_inx(), chk.last ? op_c1(0) : op_bank(0), XB, rb);
@@ -413,16 +493,19 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         // conv1 (stride 1): y1 = act(conv1(h) + b1)
         LzChunk chk;
         const int nfi = lz_nf(Ti);
+        auto r0_c1 = [=](const LzChunk& ch) __attribute__((always_inline)) { return LZ_ZR + 16 * ch.f0 - P; };
+        auto nr_c1 = [=](const LzChunk&) __attribute__((always_inline)) { return 127 + ks + 2; };
+        LzPipe<PREC, 136> pipe1(WB, nfi, 127 + ks + 2);
+        pipe1.prime(imgh, r0_c1, nr_c1);
         for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
-            __syncthreads();
-            lz_stage<PREC>(WB, imgh, LZ_ZR + n0 - P, 127 + ks + 2);
-            __syncthreads();
+            const char* SB = pipe1.next(k, chk, imgh, r0_c1, nr_c1);
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Ti - 1) - n0;
             f32x4 acc[2][NF];
             zero_acc(acc);
-            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c1(l), chk.last ? op_c2(l) : op_c1(l), WB, rb);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c1(l), chk.last ? op_c2(l) : op_c1(l), SB, rb);
+            pipe1.issue_next(k, imgh, r0_c1, nr_c1);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int t = n0 + 16 * f + c;
@@ -462,17 +545,20 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             if (2 * t + 1 < Ti) return (a + *lz_fl(hin, 2 * t + 1, w, i)) / 2.f;
             return a;
         };
+        auto r0_c2 = [=](const LzChunk& ch) __attribute__((always_inline)) { return LZ_ZR + s * 16 * ch.f0 - P; };
+        auto nr_c2 = [=](const LzChunk&) __attribute__((always_inline)) { return s * 127 + ks + 2; };
+        LzPipe<PREC, 264> pipe2(WB, nfo, s * 127 + ks + 2);
+        pipe2.prime(imgy, r0_c2, nr_c2);
         for (int k = 0; lz_chunk(k, nfo, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
-            __syncthreads();
-            lz_stage<PREC>(WB, imgy, LZ_ZR + s * n0 - P, s * 127 + ks + 2);
-            __syncthreads();
+            const char* SB = pipe2.next(k, chk, imgy, r0_c2, nr_c2);
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = s * (min(n0 + 16 * f + c, To - 1) - n0);
             f32x4 acc[2][NF];
             zero_acc(acc);
             const AOp nxt = chk.last ? (!lastblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l))) : op_c2(l);
-            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l), nxt, WB, rb);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l), nxt, SB, rb);
+            pipe2.issue_next(k, imgy, r0_c2, nr_c2);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int t = n0 + 16 * f + c;
@@ -644,13 +730,19 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         // conv2^T over padded positions v = n - 16 of the Ti input frames, * act'(y1) -> imgg2
         const int nfc = lz_nf(Ti + 16 + P);
         LzChunk chk;
+        // rows of a chunk's input-gradient window: padded positions v in [vlo, vhi] + taps
+        auto r0_g = [=](const LzChunk& ch) __attribute__((always_inline)) {
+            return LZ_ZR + max(16 * ch.f0 - 16, -P) + P - ks - 1;
+        };
+        auto nr_g = [=](const LzChunk& ch) __attribute__((always_inline)) {
+            return min(16 * ch.f0 + 111, Ti + P - 1) - max(16 * ch.f0 - 16, -P) + ks + 2;
+        };
+        LzPipe<PREC, 136> pipeg(WB, nfc, 127 + ks + 2);
+        pipeg.prime(imgg, r0_g, nr_g);
         for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
-            const int vlo = max(n0 - 16, -P), vhi = min(n0 + 111, Ti + P - 1);
-            const int r0 = LZ_ZR + vlo + P - ks - 1;
-            __syncthreads();
-            lz_stage<PREC>(WB, imgg, r0, vhi - vlo + ks + 2);
-            __syncthreads();
+            const int r0 = r0_g(chk);
+            const char* SB = pipeg.next(k, chk, imgg, r0_g, nr_g);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
@@ -658,8 +750,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             }
             f32x4 acc[2][NF];
             zero_acc(acc);
-            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c2T(l), chk.last ? op_c1T(l) : op_c2T(l), WB, rb);
+            fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c2T(l), chk.last ? op_c1T(l) : op_c2T(l), SB, rb);
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
+            pipeg.issue_next(k, imgg, r0_g, nr_g);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int F = chk.f0 + f - 1, t = 16 * F + c;   // frame of the column
@@ -686,13 +779,12 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         char* nimg = l > 0 ? imgg : imgp;
         float* gprev = gh[cur];
         float* gnew = gh[cur ^ 1];
+        LzPipe<PREC, 136> pipeg2(WB, nfc, 127 + ks + 2);
+        pipeg2.prime(imgg2, r0_g, nr_g);
         for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
-            const int vlo = max(n0 - 16, -P), vhi = min(n0 + 111, Ti + P - 1);
-            const int r0 = LZ_ZR + vlo + P - ks - 1;
-            __syncthreads();
-            lz_stage<PREC>(WB, imgg2, r0, vhi - vlo + ks + 2);
-            __syncthreads();
+            const int r0 = r0_g(chk);
+            const char* SB = pipeg2.next(k, chk, imgg2, r0_g, nr_g);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
@@ -703,11 +795,12 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             const AOp nxt = chk.last ? (l > 0 ? op_c2T(l - 1) : op_inTx()) : op_c1T(l);
             if (chk.last && l == 0) {
                 // the bank phase runs on a 5-tile ring: refill the 2-tile ring with a dummy
-                fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), op_c1T(l), WB, rb);
+                fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), op_c1T(l), SB, rb);
             } else {
-                fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), nxt, WB, rb);
+                fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), nxt, SB, rb);
             }
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
+            pipeg2.issue_next(k, imgg2, r0_g, nr_g);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int F = chk.f0 + f - 1, t = 16 * F + c;
@@ -798,7 +891,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         } else {
             fz_gemm<PREC, 5, LZ_CHF, FZ_C, 1>(accx, IC<CHF>{}, ring5, op_inTx(), op_inTb(0), GP, rbx);
         }
-        for (int kb = 0; kb < nb; ++kb) {
+        auto bank_step = [&](auto KB) __attribute__((always_inline)) {
+            const int kb = KB;
             const int kk = kb + 1, pl = kk / 2;
             // g(b_k) for this wave's 32 bank channels over the window = (W_in[:, kb]^T g_pre0) * act'(b_k)
             f32x4 acc[2][NFW];
@@ -835,7 +929,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                 fz_gemm<PREC, 5, LZ_CHF, FZ_C, -1>(accx, IC<CHF>{}, ring5, op_bankT(kb), nxt, GBK, rb);
             }
             __syncthreads();
-        }
+        };
+        for (int kb = 0; kb < nb; ++kb) bank_step(kb);
         if (!chk.last) {   // ring5 now holds op_bankT(nb-1) prefetches; the next chunk starts at in_x^T
             ring_fill(ring5, op_inTx());
         }
@@ -856,25 +951,44 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             }
             __syncthreads();
         }
-        // owned interior columns: t = n - 4 in [0, T)
-        for (int idx = tid; idx < FZ_CIN * CH; idx += 256) {
-            const int ci = idx / CH, col = idx - ci * CH;
-            const int n = n0 + col, t = n - 4;
-            if (!chk.owns(n) || t < 0 || t >= T) continue;
-            const float gsum = R0[ci * CH + col] + R1[ci * CH + col];
-            const size_t q = xb + (size_t)ci * T + t;
-            if (A.gx_out) {
-                A.gx_out[q] = gsum;
-                continue;
+        // owned interior columns: t = n - 4 in [0, T).  UB elements per thread per batch, all
+        // their state loads issued before any arithmetic (one memory round trip per batch)
+        constexpr int UB = 4;
+        for (int i0 = 0; i0 < FZ_CIN * CH; i0 += 256 * UB) {
+            size_t qv[UB];
+            bool ok[UB];
+            float gs[UB], P[UB], M[UB], V[UB], X[UB];
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                const int idx = i0 + tid + 256 * u;
+                const int ci = idx / CH, col = idx - ci * CH;
+                const int n = n0 + col, t = n - 4;
+                ok[u] = idx < FZ_CIN * CH && chk.owns(n) && t >= 0 && t < T;
+                qv[u] = xb + (size_t)min(ci, FZ_CIN - 1) * T + min(max(t, 0), T - 1);
+                gs[u] = idx < FZ_CIN * CH ? R0[ci * CH + col] + R1[ci * CH + col] : 0.f;
+                if (adam) {
+                    P[u] = Ad.ptb[qv[u]];
+                    M[u] = Ad.m[qv[u]];
+                    V[u] = Ad.v[qv[u]];
+                    X[u] = Ad.vc[qv[u]];
+                }
             }
-            float p = Ad.ptb[q], mm = Ad.m[q], vv = Ad.v[q];
-            float g, ad;
-            adam_elem<PREC>(Ad, S, gsum, Ad.vc[q], p, mm, vv, g, ad);
-            if (Ad.grad0 && step == 1) Ad.grad0[q] = g;
-            Ad.ptb[q] = p;
-            Ad.m[q] = mm;
-            Ad.v[q] = vv;
-            Ad.adv[q] = ad;
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                if (!ok[u]) continue;
+                const size_t q = qv[u];
+                if (!adam) {
+                    A.gx_out[q] = gs[u];
+                    continue;
+                }
+                float p = P[u], mm = M[u], vv = V[u], g, ad;
+                adam_elem<PREC>(Ad, S, gs[u], X[u], p, mm, vv, g, ad);
+                if (Ad.grad0 && step == 1) Ad.grad0[q] = g;
+                Ad.ptb[q] = p;
+                Ad.m[q] = mm;
+                Ad.v[q] = vv;
+                Ad.adv[q] = ad;
+            }
         }
     }
 }
