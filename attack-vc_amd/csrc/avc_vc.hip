@@ -39,11 +39,35 @@ struct StdDec {
     static constexpr int nf(int frames) { return (frames + 15) / 16; }
 };
 
-// stash slot of (half, fragment f, tile i) for this wave: 4 floats per lane, one 1 KiB
-// coalesced store per (half, f, i); nfq = fragments of the layer's frames
-__device__ __forceinline__ float* dz_stash(const DecArgs& A, int b, int q, int half, int nfq, int f, int i, int w) {
-    return A.stash + (size_t)b * A.stash_per_utt + A.stash_off[q] +
-           ((size_t)(((half * nfq + f) * 4 + w) * 2 + i) * 64 + (threadIdx.x & 63)) * 4;
+// stash slot of (half, fragment f, tile i) for this wave: 4 values per lane, one coalesced
+// store per (half, f, i); nfq = fragments of the layer's frames.  fp32 mode stores fp32 (1 KiB
+// per store); bf16 mode stores the normalised activations as bf16 (512 B: the stash is the
+// Decoder's dominant HBM stream, written by the forward and read back by the backward)
+__device__ __forceinline__ size_t dz_slot(const DecArgs& A, int b, int q, int half, int nfq, int f, int i, int w,
+                                          int per4) {
+    return (size_t)b * A.stash_per_utt / per4 + A.stash_off[q] / per4 +
+           ((size_t)(((half * nfq + f) * 4 + w) * 2 + i) * 64 + (threadIdx.x & 63));
+}
+template <int PREC>
+__device__ __forceinline__ void dz_stash_put(const DecArgs& A, int b, int q, int half, int nfq, int f, int i, int w,
+                                             f32x4 v) {
+    if constexpr (PREC == PREC_F32) {
+        reinterpret_cast<f32x4*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)] = v;
+    } else {
+        bf16x4 h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = (__bf16)v[e];
+        reinterpret_cast<bf16x4*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)] = h;
+    }
+}
+template <int PREC>
+__device__ __forceinline__ f32x4 dz_stash_get(const DecArgs& A, int b, int q, int half, int nfq, int f, int i, int w) {
+    if constexpr (PREC == PREC_F32) {
+        return reinterpret_cast<const f32x4*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)];
+    } else {
+        const bf16x4 h = reinterpret_cast<const bf16x4*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)];
+        return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    }
 }
 
 // InstanceNorm over the two halves of a shuffled layer (2*T frames per channel)
@@ -171,7 +195,7 @@ __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
         for (int f = 0; f < NF; ++f)
             if (f < nfq)
 #pragma unroll
-                for (int i = 0; i < 2; ++i) *reinterpret_cast<f32x4*>(dz_stash(A, b, q, half, nfq, f, i, w)) = v[i][f];
+                for (int i = 0; i < 2; ++i) dz_stash_put<PREC>(A, b, q, half, nfq, f, i, w, v[i][f]);
         if (half == 0 && c == 0)
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -499,7 +523,7 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
             for (int f = 0; f < NF; ++f) {
                 if (f >= nfq) continue;
                 const bool in = 16 * f + c < T;
-                yh0[f] = *reinterpret_cast<const f32x4*>(dz_stash(A, b, q, 0, nfq, f, i, w));
+                yh0[f] = dz_stash_get<PREC>(A, b, q, 0, nfq, f, i, w);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float z = g0[i][f][r] * act_d(yh0[f][r] * sd[r] + mn[r], act);
@@ -510,7 +534,7 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
                     }
                 }
                 if (H == 2) {
-                    yh1[f] = *reinterpret_cast<const f32x4*>(dz_stash(A, b, q, 1, nfq, f, i, w));
+                    yh1[f] = dz_stash_get<PREC>(A, b, q, 1, nfq, f, i, w);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float z = g1[i][f][r] * act_d(yh1[f][r] * sd[r] + mn[r], act);
