@@ -37,7 +37,7 @@ def libname(k):
     base, args = k.split("<", 1)
     first = args.rstrip(">").split(",")[0].strip()
     if first in ("0", "1") and base not in ("se_head_v",):
-        return f"{base}<{'bf16' if first == '1' else 'fp32'}>"
+        return f"{base}<{'bf16' if first == '1' else 'f32'}>"
     return k
 
 
