@@ -875,7 +875,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     auto op_bankT = [&](int kb) __attribute__((always_inline)) {
         return aop(A.w.bankT[kb], 0, 5, (kb + 1) * SPT, (kb + 1) * SPW, LG, SPW - 1, SPT, w * SPW);
     };
-    ARing<5> ring5;
+    ARing<5, 2> ring5;   // 2 slots: see ARing
     {   // x passthrough of the cat: W_in[:, x block]^T g_pre0 (interior columns only)
 #pragma unroll
         for (int f = 0; f < NF; ++f) {

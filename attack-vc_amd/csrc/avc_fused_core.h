@@ -103,9 +103,14 @@ __device__ __forceinline__ const f32x4* a_step(const AOp& o, int s) {
 // Four K steps of A in flight: slot u of the ring holds step s+u.  A GEMM refills a slot
 // right after using it, and the refills that run past its last step fetch the NEXT
 // GEMM's first steps instead, so no GEMM starts with an exposed L2/MALL round trip.
-template <int MTR>
+// RD slots: 4 by default; 2 where a step already carries many MFMAs (the bank backward's
+// 5-tile x 9-fragment steps: 720 MFMA cycles per step cover an L2 round trip with one
+// spare slot, and the 4-slot ring's 80 extra VGPRs made the compiler collapse the ring into
+// load -> wait -> use on every step)
+template <int MTR, int RD = 4>
 struct ARing {
-    f32x4 a[4][MTR];
+    static_assert(RD == 2 || RD == 4, "ring depth");
+    f32x4 a[RD][MTR];
 };
 // slot <- step s of A (s < A.ns) or step s - A.ns of N; branch-free (uniform selects);
 // tiles beyond an operand's own count re-read its last tile (an L1 hit, never used)
@@ -128,13 +133,13 @@ __device__ __forceinline__ void ring_load(f32x4 (&slot)[MTR], const AOp& A, cons
     for (int i = 0; i < MTR; ++i) slot[i] = f32x4{0.001f * s, 0.f, 0.f, 0.f};
 #endif
 }
-template <int MTR>
-__device__ __forceinline__ void ring_fill(ARing<MTR>& R, const AOp& A) {
+template <int MTR, int RD>
+__device__ __forceinline__ void ring_fill(ARing<MTR, RD>& R, const AOp& A) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) ring_load<MTR>(R.a[u], A, A, u);
+    for (int u = 0; u < RD; ++u) ring_load<MTR>(R.a[u], A, A, u);
 }
 
-// acc[MT][NF] += A x B; the ring holds A's steps 0..3 on entry and N's steps 0..3 on exit.
+// acc[MT][NF] += A x B; the ring holds A's steps 0..RD-1 on entry and N's steps 0..RD-1 on exit.
 //   B  : LDS base of the operand image; rb[f] = row of tap 0 for this lane's column
 //   DJ : +1 forward (row = rb + j), -1 adjoint (row = rb - j)
 // B fragments are read one step ahead into two alternating register sets.  The loop
@@ -143,8 +148,8 @@ __device__ __forceinline__ void ring_fill(ARing<MTR>& R, const AOp& A) {
 // waitcnt pass sees a fixed number of loads in flight.
 // NFC > 0: the live fragment count is the compile-time NFC (straight-line K loop);
 // NFC == 0: up to NF fragments, the first `nf` live (runtime guards; generic shapes).
-template <int PREC, int MT, int MTR, int NF, int NFC, int CINB, int DJ>
-__device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing<MTR>& R, const AOp& A,
+template <int PREC, int MT, int MTR, int RD, int NF, int NFC, int CINB, int DJ>
+__device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing<MTR, RD>& R, const AOp& A,
                                              const AOp& N, const char* B, const int (&rb)[NF]) {
     static_assert(MT <= MTR, "ring narrower than the GEMM");
     constexpr int NL = NFC ? NFC : NF;                 // fragments the loops run over
@@ -177,73 +182,84 @@ __device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing
     };
     f32x4 bA[NL], bB[NL];
     read_b(bA, 0);
-    const int nfull = ns & ~3;
+    const int nfull = ns & ~(RD - 1);
 #pragma unroll 1
-    for (int s = 0; s < nfull; s += 4) {
+    for (int s = 0; s < nfull; s += RD) {
         read_b(bB, s + 1);
         mma_all(R.a[0], bA);
-        ring_load<MTR>(R.a[0], A, N, s + 4);
+        ring_load<MTR>(R.a[0], A, N, s + RD);
         read_b(bA, s + 2);
         mma_all(R.a[1], bB);
-        ring_load<MTR>(R.a[1], A, N, s + 5);
-        read_b(bB, s + 3);
-        mma_all(R.a[2], bA);
-        ring_load<MTR>(R.a[2], A, N, s + 6);
-        read_b(bA, s + 4);
-        mma_all(R.a[3], bB);
-        ring_load<MTR>(R.a[3], A, N, s + 7);
+        ring_load<MTR>(R.a[1], A, N, s + RD + 1);
+        if constexpr (RD == 4) {
+            read_b(bB, s + 3);
+            mma_all(R.a[2], bA);
+            ring_load<MTR>(R.a[2], A, N, s + 6);
+            read_b(bA, s + 4);
+            mma_all(R.a[3], bB);
+            ring_load<MTR>(R.a[3], A, N, s + 7);
+        }
     }
-    // remainder (0..3 steps): slots hold steps nfull..nfull+3 (slot u = step nfull+u),
+    // remainder (0..RD-1 steps): slots hold steps nfull..nfull+RD-1 (slot u = step nfull+u),
     // bA holds step nfull.  Afterwards rotate so that slot u = N's step u again.
     const int rem = ns - nfull;
 #if AVC_FZ_ABLATE & 4
     // debug: no cross-GEMM prefetch -- finish this GEMM's own steps, then load N afresh
     if (rem >= 1) mma_all(R.a[0], bA);
-    if (rem >= 2) {
-        read_b(bB, nfull + 1);
-        mma_all(R.a[1], bB);
-    }
-    if (rem >= 3) {
-        read_b(bA, nfull + 2);
-        mma_all(R.a[2], bA);
+    if constexpr (RD == 4) {
+        if (rem >= 2) {
+            read_b(bB, nfull + 1);
+            mma_all(R.a[1], bB);
+        }
+        if (rem >= 3) {
+            read_b(bA, nfull + 2);
+            mma_all(R.a[2], bA);
+        }
     }
     ring_fill(R, N);
     return;
 #endif
     if (rem == 0) return;
     mma_all(R.a[0], bA);
-    ring_load<MTR>(R.a[0], A, N, nfull + 4);
-    if (rem >= 2) {
-        read_b(bB, nfull + 1);
-        mma_all(R.a[1], bB);
-        ring_load<MTR>(R.a[1], A, N, nfull + 5);
+    ring_load<MTR>(R.a[0], A, N, nfull + RD);
+    if constexpr (RD == 4) {
+        if (rem >= 2) {
+            read_b(bB, nfull + 1);
+            mma_all(R.a[1], bB);
+            ring_load<MTR>(R.a[1], A, N, nfull + 5);
+        }
+        if (rem >= 3) {
+            read_b(bA, nfull + 2);
+            mma_all(R.a[2], bA);
+            ring_load<MTR>(R.a[2], A, N, nfull + 6);
+        }
     }
-    if (rem >= 3) {
-        read_b(bA, nfull + 2);
-        mma_all(R.a[2], bA);
-        ring_load<MTR>(R.a[2], A, N, nfull + 6);
-    }
-    // a GEMM shorter than the ring (ns < 4) entered with slots u >= ns holding clamped
+    // a GEMM shorter than the ring (ns < RD) entered with slots u >= ns holding clamped
     // copies of its own last step (its predecessor could not know this GEMM's successor):
     // those slots get N's steps u - rem now
     if (nfull == 0)
-        for (int u = rem; u < 4; ++u) {
+        for (int u = rem; u < RD; ++u) {
 #pragma unroll
-            for (int v = 0; v < 4; ++v)
+            for (int v = 0; v < RD; ++v)
                 if (v == u) ring_load<MTR>(R.a[v], N, N, u - rem);
         }
-    // slot u now holds step nfull + u + 4*(u < rem) of the A|N stream, i.e. N's step
-    // (u - rem) mod 4: rotate left by rem
-    f32x4 t[4][MTR];
+    // slot u now holds step nfull + u + RD*(u < rem) of the A|N stream, i.e. N's step
+    // (u - rem) mod RD: rotate left by rem
+    f32x4 t[RD][MTR];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < RD; ++u)
 #pragma unroll
         for (int i = 0; i < MTR; ++i) t[u][i] = R.a[u][i];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < RD; ++u)
 #pragma unroll
-        for (int i = 0; i < MTR; ++i)
-            R.a[u][i] = rem == 1 ? t[(u + 1) & 3][i] : (rem == 2 ? t[(u + 2) & 3][i] : t[(u + 3) & 3][i]);
+        for (int i = 0; i < MTR; ++i) {
+            if constexpr (RD == 2) {
+                R.a[u][i] = t[(u + 1) & 1][i];   // rem == 1
+            } else {
+                R.a[u][i] = rem == 1 ? t[(u + 1) & 3][i] : (rem == 2 ? t[(u + 2) & 3][i] : t[(u + 3) & 3][i]);
+            }
+        }
 }
 
 // Diagnostic build only (-DAVC_FZ_PHASES): per-wave cycle stamps at phase boundaries,
@@ -277,16 +293,16 @@ using IC = std::integral_constant<int, V>;
 
 // fz_gemm: the fragment count is either a compile-time IC<N> (specialised shapes) or a
 // runtime int (generic shapes)
-template <int PREC, int MT, int NF, int CINB, int DJ, int MTR, int NFC>
-__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], IC<NFC>, ARing<MTR>& R, const AOp& A, const AOp& N,
+template <int PREC, int MT, int NF, int CINB, int DJ, int MTR, int RD, int NFC>
+__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], IC<NFC>, ARing<MTR, RD>& R, const AOp& A, const AOp& N,
                                         const char* B, const int (&rb)[NF]) {
     static_assert(NFC >= 1 && NFC <= NF, "fragment count");
-    fz_gemm_impl<PREC, MT, MTR, NF, NFC, CINB, DJ>(acc, NFC, R, A, N, B, rb);
+    fz_gemm_impl<PREC, MT, MTR, RD, NF, NFC, CINB, DJ>(acc, NFC, R, A, N, B, rb);
 }
-template <int PREC, int MT, int NF, int CINB, int DJ, int MTR>
-__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], int nf, ARing<MTR>& R, const AOp& A, const AOp& N,
+template <int PREC, int MT, int NF, int CINB, int DJ, int MTR, int RD>
+__device__ __forceinline__ void fz_gemm(f32x4 (&acc)[MT][NF], int nf, ARing<MTR, RD>& R, const AOp& A, const AOp& N,
                                         const char* B, const int (&rb)[NF]) {
-    fz_gemm_impl<PREC, MT, MTR, NF, 0, CINB, DJ>(acc, nf, R, A, N, B, rb);
+    fz_gemm_impl<PREC, MT, MTR, RD, NF, 0, CINB, DJ>(acc, nf, R, A, N, B, rb);
 }
 
 template <int I, int N, class F>
@@ -420,10 +436,15 @@ struct MaskAcc {
 // issued ahead of the GEMM that precedes their use.
 struct MaskRd {
     unsigned lo = 0, hi = 0;
+    // The scheduling barrier keeps the load where it is written (ahead of the GEMM that
+    // precedes the words' use): the scheduler otherwise sank it to just before the use, where
+    // its wait (vmcnt(0): the youngest load) also drained the GEMM's whole weight prefetch ring
+    // -- measured 7-9k cycles per bank kernel in the backward's bank phase.
     __device__ __forceinline__ void load(const u64* base) {
         const u64 v = base[threadIdx.x & 63];
         lo = (unsigned)v;
         hi = (unsigned)(v >> 32);
+        __builtin_amdgcn_sched_barrier(0);
     }
     // act'(y) of element (i, f, r): 1 where y > 0, else 0 (ReLU) or 0.01 (LeakyReLU)
     __device__ __forceinline__ float act(int i, int f, int r, int actk) const {

@@ -842,7 +842,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     constexpr int CHF = LzBank<PREC>::CHF, CH = 16 * CHF;
     constexpr int NFW = CHF + 1;                        // g(b_k) window: frames n0-16 .. n0+CH-1
     constexpr int ZPB = 8;
-    ARing<5> ring5;
+    ARing<5, 2> ring5;   // 2 slots: see ARing
     ring_fill(ring5, op_inTx());
     lz_zero_rows<PREC>(imgp, 0, LZ_ZR);
     lz_zero_rows<PREC>(imgp, LZ_ZR + T, LZ_ZR);
