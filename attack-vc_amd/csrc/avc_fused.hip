@@ -875,7 +875,20 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     auto op_bankT = [&](int kb) __attribute__((always_inline)) {
         return aop(A.w.bankT[kb], 0, 5, (kb + 1) * SPT, (kb + 1) * SPW, LG, SPW - 1, SPT, w * SPW);
     };
-    ARing<5, 2> ring5;   // 2 slots: see ARing
+    // The bank phase is wave-local: wave w writes g(b_k) for ITS 32 bank channels into GBK and
+    // its bank_k^T GEMM reads only those channels (K split over waves), and g_pre0 (GP) is
+    // read-only here -- so no workgroup barrier between the phases of a bank kernel: a wave's
+    // own LDS accesses are executed in order, and a compiler fence keeps them in program order.
+    // The in_conv^T GEMMs (4 bf16 K steps) take their whole A operand from registers loaded one
+    // GEMM ahead (ARes); the wide 2-slot ring carries only the bank_k^T steps, prefetched across
+    // in_conv^T and the gate.
+    // 2 slots: see ARing (a fully unrolled 2- or 3-slot variant of this phase spilled and ran
+    // slower: 99 -> 107 us per launch, A/B)
+    ARing<5, 2> ring5;
+    constexpr int NSI = FZ_C / KS;              // in_conv^T K steps
+    ARes<NSI, 2> resi;
+    MaskRd mbn;                                 // ReLU' words of the next bank kernel, a GEMM ahead
+    mbn.load(mwords(0));
     {   // x passthrough of the cat: W_in[:, x block]^T g_pre0 (interior columns only)
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
@@ -884,7 +897,8 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         }
         const AOp opx = aop(A.w.inT_x, 0, 5, SPT, SPW, 30, -1, 0, w * SPW);
         ring_fill(ring5, opx);
-        fz_gemm<PREC, 5, NF, FZ_C, 1>(accx, nfx, ring5, opx, op_inTb(0), GP, rb);
+        res_load(resi, op_inTb(0));
+        fz_gemm<PREC, 5, NF, FZ_C, 1>(accx, nfx, ring5, opx, op_bankT(0), GP, rb);
     }
     FZ_PH();
     auto bank_bwd = [&](auto KB) __attribute__((always_inline)) {
@@ -893,12 +907,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         // g(b_k) for this wave's 32 bank channels = (W_in[:, kb]^T g_pre0) * act'(b_k)
         f32x4 acc[2][8];
         zero_acc(acc);
-        MaskRd mb;
-        mb.load(mwords(kb));
+        const MaskRd mb = mbn;
         int rt[8];
 #pragma unroll
         for (int f = 0; f < 8; ++f) rt[f] = ZP + min(16 * f + c, T - 1);
-        fz_gemm<PREC, 2, 8, FZ_C, 1>(acc, nf0, ring5, op_inTb(kb), op_bankT(kb), GP, rt);
+        fz_gemm_res<PREC, 2, 8, NSI, FZ_C, 1>(acc, nf0, resi, GP, rt);
         FZ_PH();
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -911,7 +924,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                 const int t = 16 * f + c;
                 if (t < T) st4<PREC>(GBK + (ZPB + t) * RS + (ch0 + 16 * i) * ESZ, v);
             }
-        __syncthreads();
+        asm volatile("" ::: "memory");   // wave-local hand-off (see above): program order only
+        if (kb + 1 < nb) {
+            res_load(resi, op_inTb(kb + 1));
+            mbn.load(mwords(kb + 1));
+        }
         FZ_PH();
         // bank_k^T over this wave's channel quarter: rows q = v + pl - j of g(b_k)
 #pragma unroll
@@ -919,8 +936,9 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
             const int n = 16 * f + c;
             rb[f] = ZPB + (n < T + 2 * EB ? vpos(n, T, EB) : 0) + pl;
         }
-        fz_gemm<PREC, 5, NF, FZ_C, -1>(accx, nfx, ring5, op_bankT(kb), kb + 1 < nb ? op_inTb(kb + 1) : op_bankT(kb), GBK, rb);
-        __syncthreads();
+        const AOp opn = kb + 1 < nb ? op_bankT(kb + 1) : op_bankT(kb);
+        fz_gemm<PREC, 5, NF, FZ_C, -1>(accx, nfx, ring5, op_bankT(kb), opn, GBK, rb);
+        asm volatile("" ::: "memory");
         FZ_PH();
     };
     if constexpr (STD != 0) {
@@ -970,6 +988,10 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         for (int q = tid; q < FZ_CIN * T / 4; q += 256) gx[q] = R04[rq(q)] + R14[rq(q)];
         return;
     }
+    // Adam tail (reads ptb, m, v, vc, writes ptb, m, v, adv: 320 KB per utterance, every
+    // workgroup at once -- the chip's burst rate bounds it).  Hoisting the reads ahead of the
+    // fold / cross-wave sum measured no gain: the loaded registers were parked in AGPRs at once
+    // (a vmcnt wait there) under the bank phase's register pressure.
     const AdamArgs& Ad = A.adam;
     const float eps = A.scal[0];
     if (A.losses && tid == 0) {   // the fused head's loss of this iteration -> history row step-1
@@ -990,53 +1012,40 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     f32x4* __restrict__ g04 = Ad.grad0 && step == 1 ? reinterpret_cast<f32x4*>(Ad.grad0) + base4 : nullptr;
     const f32x4* R04 = reinterpret_cast<const f32x4*>(R0);
     const f32x4* R14 = reinterpret_cast<const f32x4*>(R1);
-    // 16-byte accesses; a batch's loads all issued before its arithmetic (one HBM round
-    // trip per batch instead of one per element)
+    // one batch of 16-byte accesses covers the utterance (80 x T / 4 <= 256 * AB at T <= 128);
+    // all its loads are issued before its arithmetic (one HBM round trip)
     const int n4 = FZ_CIN * T / 4;
-    constexpr int AB = 10;                      // f32x4 per thread per batch (T = 128: one batch)
-    for (int q0 = 0; q0 < n4; q0 += 256 * AB) {
-        f32x4 P[AB], M[AB], V[AB], X[AB];
+    constexpr int AB = 10;
+    f32x4 sP[AB], sM[AB], sV[AB], sX[AB];
 #pragma unroll
-        for (int k = 0; k < AB; ++k) {
-            const int q = min(q0 + tid + 256 * k, n4 - 1);
-            P[k] = ptb4[q];
-            M[k] = m4[q];
-            V[k] = v4[q];
-            X[k] = vc4[q];
+    for (int k = 0; k < AB; ++k) {
+        const int q = min(tid + 256 * k, n4 - 1);
+        sP[k] = ptb4[q];
+        sM[k] = m4[q];
+        sV[k] = v4[q];
+        sX[k] = vc4[q];
+    }
+#pragma unroll
+    for (int k = 0; k < AB; ++k) {
+        const int q = tid + 256 * k;
+        if (q >= n4) continue;
+        const f32x4 gsum = R04[rq(q)] + R14[rq(q)];
+        f32x4 p = sP[k], mm = sM[k], vv = sV[k], g, ad;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float pe = p[e], me = mm[e], ve = vv[e], ge, ae;
+            adam_elem<PREC>(Ad, S, gsum[e], sX[k][e], pe, me, ve, ge, ae);
+            p[e] = pe;
+            mm[e] = me;
+            vv[e] = ve;
+            g[e] = ge;
+            ad[e] = ae;
         }
-#pragma unroll
-        for (int k = 0; k < AB; ++k) {
-            const int q = q0 + tid + 256 * k;
-            if (q >= n4) continue;
-            const f32x4 gsum = R04[rq(q)] + R14[rq(q)];
-            f32x4 p = P[k], mm = M[k], vv = V[k], g, ad;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-#if AVC_FZ_ABLATE & 8
-                // timing only: the tail without its transcendental / IEEE-division cost
-                const float th = p[e] * 0.5f;
-                g[e] = (gsum[e] * eps) * (1.f - th * th);
-                mm[e] = mm[e] + Ad.b1c * (g[e] - mm[e]);
-                vv[e] = vv[e] * Ad.b2;
-                vv[e] = vv[e] + Ad.b2c * g[e] * g[e];
-                p[e] = p[e] + nstep * (mm[e] * (vv[e] * bc2s + Ad.adam_eps));
-                ad[e] = X[k][e] + eps * p[e] * 0.25f;
-#else
-                float pe = p[e], me = mm[e], ve = vv[e], ge, ae;
-                adam_elem<PREC>(Ad, S, gsum[e], X[k][e], pe, me, ve, ge, ae);
-                p[e] = pe;
-                mm[e] = me;
-                vv[e] = ve;
-                g[e] = ge;
-                ad[e] = ae;
-#endif
-            }
-            if (g04) g04[q] = g;
-            ptb4[q] = p;
-            m4[q] = mm;
-            v4[q] = vv;
-            adv4[q] = ad;
-        }
+        if (g04) g04[q] = g;
+        ptb4[q] = p;
+        m4[q] = mm;
+        v4[q] = vv;
+        adv4[q] = ad;
     }
     FZ_PH();
     FZ_PH_DUMP("bwd");

@@ -33,6 +33,8 @@ struct Fz<PREC_BF16> {
 extern __shared__ __attribute__((aligned(16))) char fz_lds[];
 
 typedef unsigned long long u64;
+template <int V>
+using IC = std::integral_constant<int, V>;
 
 
 __device__ __forceinline__ f32x4 lds16(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
@@ -262,6 +264,49 @@ __device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing
         }
 }
 
+// A GEMM whose whole A operand (NS K steps x MT tiles, identity step map) sits in registers
+// before it starts: loaded by res_load one GEMM ahead, so a short GEMM (the bank backward's
+// in_conv^T: 4 bf16 steps) never waits on L2 and needs no slot of the wide ring.
+template <int NS, int MT>
+struct ARes {
+    f32x4 a[NS][MT];
+};
+template <int NS, int MT>
+__device__ __forceinline__ void res_load(ARes<NS, MT>& R, const AOp& A) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+            R.a[s][i] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
+                (const __attribute__((address_space(1))) f32x4*)(A.p + (size_t)s * 64 + (size_t)i * A.amt));
+}
+template <int PREC, int MT, int NF, int NS, int CINB, int DJ, int NFC>
+__device__ __forceinline__ void fz_gemm_res(f32x4 (&acc)[MT][NF], IC<NFC>, const ARes<NS, MT>& R, const char* B,
+                                            const int (&rb)[NF]) {
+    using E = typename Fz<PREC>::E;
+    constexpr int RS = Fz<PREC>::RS;
+    constexpr int VE = 16 / (int)sizeof(E);
+    constexpr int KS = 4 * VE;
+    const int kq = (threadIdx.x & 63) >> 4;
+    auto read_b = [&](f32x4 (&bs)[NFC], int s) __attribute__((always_inline)) {
+        const int kl = KS * s + VE * kq;
+        const int j = kl / CINB, ci = kl - j * CINB;
+        const char* Bs = B + ci * (int)sizeof(E) + DJ * j * RS;
+#pragma unroll
+        for (int f = 0; f < NFC; ++f) bs[f] = lds16(Bs + rb[f] * RS);
+    };
+    f32x4 b[2][NFC];
+    read_b(b[0], 0);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s + 1 < NS) read_b(b[(s + 1) & 1], s + 1);   // next step's B ahead of this step's MFMAs
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int f = 0; f < NFC; ++f) mma<PREC>(acc[i][f], R.a[s][i], b[s & 1][f]);
+    }
+}
+
 // Diagnostic build only (-DAVC_FZ_PHASES): per-wave cycle stamps at phase boundaries,
 // printed by workgroup 0 at the end of the kernel (scripts/dbg/phases.sh).
 #ifdef AVC_FZ_PHASES
@@ -288,8 +333,6 @@ __device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing
     } while (0)
 #endif
 
-template <int V>
-using IC = std::integral_constant<int, V>;
 
 // fz_gemm: the fragment count is either a compile-time IC<N> (specialised shapes) or a
 // runtime int (generic shapes)
