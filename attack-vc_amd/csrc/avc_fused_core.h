@@ -44,10 +44,14 @@ __device__ __forceinline__ void st4(char* p, f32x4 v) {
     if constexpr (PREC == PREC_F32) {
         *reinterpret_cast<f32x4*>(p) = v;
     } else {
-        bf16x4 b;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
-        *reinterpret_cast<bf16x4*>(p) = b;
+        // two packed conversions (v_cvt_pk_bf16_f32 each); element-wise casts made the compiler
+        // convert one element per instruction and re-pair them with v_perm / v_alignbit
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        const bf16x2 lo = __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2);
+        const bf16x2 hi = __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2);
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<u32x2*>(p) = u32x2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
     }
 }
 
