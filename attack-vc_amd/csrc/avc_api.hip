@@ -44,6 +44,7 @@ __global__ void dec_fwd_fused(DecArgs A);
 template <int PREC, int SH>
 __global__ void dec_bwd_fused(DecArgs A);
 __global__ void dense_batched(DenseArgs D);
+__global__ void dense_mfma(DenseArgs D);
 __global__ void hdr_compose(HdrArgs A);
 __global__ void hdr_update(HdrArgs A);
 __global__ void pm_conv(PmConvArgs P);
@@ -1487,7 +1488,12 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
         return hipGetLastError();
     }
     case L_DENSE:
-        klaunch(ev, false, dense_batched, L.grid, L.block, 0, s, L.dn);
+        // fp32 MFMA tiles when the rows take 16-byte loads (K, kchunk multiples of 4; always on
+        // the AdaIN-VC config), the VALU kernel otherwise
+        if (L.dn.K % 4 == 0 && L.dn.kchunk % 4 == 0)
+            klaunch(ev, false, dense_mfma, L.grid, L.block, 0, s, L.dn);
+        else
+            klaunch(ev, false, dense_batched, L.grid, L.block, 0, s, L.dn);
         return hipGetLastError();
     case L_HDR_COMPOSE:
         klaunch(ev, false, hdr_compose, L.grid, L.block, 0, s, L.hd);

@@ -739,6 +739,75 @@ __global__ void __launch_bounds__(256) dense_batched(DenseArgs D) {
     }
 }
 
+// The same layer on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32
+// sums): a 64-row x 32-utterance tile per workgroup, wave w owns rows [16w, 16w+16) x 2
+// utterance fragments.  Lane (r, q) holds A[row r][k0+4q .. k0+4q+3] and X[col r][same k] as
+// one 16-byte load each, and the 4 MFMAs of a 16-k step take element e of both, so every
+// output sums its k in one fixed order that does not depend on the batch (shard invariance).
+// Needs K and kchunk multiples of 4 (16-byte loads); the host falls back to dense_batched.
+// The VALU kernel above ran 13.7 us per conv_affine call at B = 256 (latency / issue bound).
+__global__ void __launch_bounds__(256) dense_mfma(DenseArgs D) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r16 = l & 15, kq = l >> 4;
+    const int m0 = blockIdx.x * 64 + 16 * w, b0 = blockIdx.y * 32;
+    const int kb = blockIdx.z * D.kchunk, ke = min(D.K, kb + D.kchunk);
+    const float* Ar = D.A + (size_t)min(m0 + r16, D.M - 1) * D.K;       // rows / utterances past
+    const float* X0 = D.X + (size_t)min(b0 + r16, D.B - 1) * D.K;       // the end read a valid
+    const float* X1 = D.X + (size_t)min(b0 + 16 + r16, D.B - 1) * D.K;  // row; never stored
+    auto ld = [&](const float* row, int k) __attribute__((always_inline)) {
+        if (k + 4 <= ke) return *reinterpret_cast<const f32x4*>(row + k);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = k + e < ke ? row[k + e] : 0.f;
+        return v;
+    };
+    constexpr int U = 4;                        // 16-k steps per chunk; the next chunk is in flight
+    f32x4 ca[U], c0[U], c1[U], na[U], n0[U], n1[U];
+    auto load = [&](int s0, f32x4 (&a)[U], f32x4 (&x0)[U], f32x4 (&x1)[U]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + 16 * (s0 + u) + 4 * kq;
+            a[u] = ld(Ar, k);
+            x0[u] = ld(X0, k);
+            x1[u] = ld(X1, k);
+        }
+    };
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const int ns = (ke - kb + 15) / 16;
+    load(0, ca, c0, c1);
+    for (int s = 0; s < ns; s += U) {
+        if (s + U < ns) load(s + U, na, n0, n1);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][e], c0[u][e], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][e], c1[u][e], acc1, 0, 0, 0);
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ca[u] = na[u];
+            c0[u] = n0[u];
+            c1[u] = n1[u];
+        }
+    }
+    // C layout: lane (r, q) holds utterance b0 + 16j + r, rows m0 + 4q + 0..3
+    const int m = m0 + 4 * kq;
+    float* Y = D.Y + (size_t)blockIdx.z * D.B * D.M;
+    f32x4 bi = {0.f, 0.f, 0.f, 0.f};
+    if (D.bias && blockIdx.z == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bi[r] = m + r < D.M ? D.bias[m + r] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int bb = b0 + 16 * j + r16;
+        if (bb >= D.B) continue;
+        const f32x4 y = (j ? acc1 : acc0) + bi;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < D.M) Y[(size_t)bb * D.M + m + r] = y[r];
+    }
+}
+
 #define AVC_DZ_INST(P, S)                                          \
     template __global__ void dec_fwd_fused<P, S>(DecArgs);        \
     template __global__ void dec_bwd_fused<P, S>(DecArgs);
