@@ -359,10 +359,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
             if constexpr (PREC == PREC_F32) {
                 v = f32x4{xv[m][0], xv[m][1], xv[m][2], xv[m][3]};
             } else {
-                bf16x8 h;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) h[e] = (__bf16)xv[m][e];
-                v = __builtin_bit_cast(f32x4, h);
+                v = pk_bf16x8([&](int e) { return xv[m][e]; });
             }
             const int cb = (2 * m + xh) * 16;
             *reinterpret_cast<f32x4*>(XB + (4 + xt) * RS + cb) = v;

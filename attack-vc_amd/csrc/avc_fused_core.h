@@ -39,19 +39,28 @@ using IC = std::integral_constant<int, V>;
 
 __device__ __forceinline__ f32x4 lds16(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
 
+// f32 -> bf16 in pairs (one v_cvt_pk_bf16_f32 each); element-wise casts made the compiler
+// convert one element per instruction and re-pair them with v_perm / v_alignbit
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+__device__ __forceinline__ u32x2 pk_bf16x4(const f32x4& v) { return u32x2{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}; }
+// 8 floats -> 8 bf16 in one 16-byte register quad (as f32x4 bits)
+template <class F>
+__device__ __forceinline__ f32x4 pk_bf16x8(F&& x) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    return __builtin_bit_cast(f32x4, u32x4{pk_bf16(x(0), x(1)), pk_bf16(x(2), x(3)), pk_bf16(x(4), x(5)), pk_bf16(x(6), x(7))});
+}
+
 template <int PREC>
 __device__ __forceinline__ void st4(char* p, f32x4 v) {
     if constexpr (PREC == PREC_F32) {
         *reinterpret_cast<f32x4*>(p) = v;
     } else {
-        // two packed conversions (v_cvt_pk_bf16_f32 each); element-wise casts made the compiler
-        // convert one element per instruction and re-pair them with v_perm / v_alignbit
-        typedef float f32x2 __attribute__((ext_vector_type(2)));
-        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-        const bf16x2 lo = __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2);
-        const bf16x2 hi = __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2);
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<u32x2*>(p) = u32x2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
+        *reinterpret_cast<u32x2*>(p) = pk_bf16x4(v);
     }
 }
 

@@ -357,10 +357,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                 v = f32x4{xs[(size_t)(4 * g) * T + t], xs[(size_t)(4 * g + 1) * T + t], xs[(size_t)(4 * g + 2) * T + t],
                           xs[(size_t)(4 * g + 3) * T + t]};
             } else {
-                bf16x8 h;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) h[e] = (__bf16)xs[(size_t)(8 * g + e) * T + t];
-                v = __builtin_bit_cast(f32x4, h);
+                v = pk_bf16x8([&](int e) { return xs[(size_t)(8 * g + e) * T + t]; });
             }
             *reinterpret_cast<f32x4*>(imgx + (size_t)(LZ_ZR + t) * GRB + 16 * g) = v;
             if (t >= 1 && t <= 4) *reinterpret_cast<f32x4*>(imgx + (size_t)(LZ_ZR - t) * GRB + 16 * g) = v;
@@ -1020,10 +1017,7 @@ __device__ __forceinline__ void lz_ct_to_img(char* img, const float* src, int T)
             v = f32x4{src[(size_t)(4 * g) * T + t], src[(size_t)(4 * g + 1) * T + t], src[(size_t)(4 * g + 2) * T + t],
                       src[(size_t)(4 * g + 3) * T + t]};
         } else {
-            bf16x8 h;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) h[e] = (__bf16)src[(size_t)(8 * g + e) * T + t];
-            v = __builtin_bit_cast(f32x4, h);
+            v = pk_bf16x8([&](int e) { return src[(size_t)(8 * g + e) * T + t]; });
         }
         *reinterpret_cast<f32x4*>(img + (size_t)(LZ_ZR + t) * Z::GRB + 16 * g) = v;
     }

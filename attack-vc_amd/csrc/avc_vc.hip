@@ -54,22 +54,9 @@ __device__ __forceinline__ void dz_stash_put(const DecArgs& A, int b, int q, int
     if constexpr (PREC == PREC_F32) {
         reinterpret_cast<f32x4*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)] = v;
     } else {
-        bf16x4 h;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) h[e] = (__bf16)v[e];
-        reinterpret_cast<bf16x4*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)] = h;
+        reinterpret_cast<u32x2*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)] = pk_bf16x4(v);
     }
 }
-template <int PREC>
-__device__ __forceinline__ f32x4 dz_stash_get(const DecArgs& A, int b, int q, int half, int nfq, int f, int i, int w) {
-    if constexpr (PREC == PREC_F32) {
-        return reinterpret_cast<const f32x4*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)];
-    } else {
-        const bf16x4 h = reinterpret_cast<const bf16x4*>(A.stash)[dz_slot(A, b, q, half, nfq, f, i, w, 4)];
-        return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
-    }
-}
-
 // InstanceNorm over the two halves of a shuffled layer (2*T frames per channel)
 template <int NF>
 __device__ __forceinline__ void inorm_rows2(f32x4 (&v0)[2][NF], f32x4 (&v1)[2][NF], int nf, int T, f32x4 (&invstd)[2]) {
@@ -176,16 +163,30 @@ __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
     ring_fill(ring, op_in());
     int rb[NF];
 
-    // AdaIN (append_cond) of IN layer q on the normalised rows: z = yhat * std + mean
-    auto adain_act = [&](f32x4 (&v)[2][NF], int q) __attribute__((always_inline)) {
+    // AdaIN (append_cond) of IN layer q on the normalised rows: z = yhat * std + mean.  The
+    // conditions (and the layer's bias) are loaded ahead of the GEMM that precedes their use,
+    // so their L2 round trip hides under it.
+    struct Cnd {
+        f32x4 mn[2], sd[2], b0[2], b1[2];
+    };
+    auto cnd_load = [&](int q, const float* bias0, const float* bias1) __attribute__((always_inline)) {
+        Cnd k;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const f32x4 mn = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
-            const f32x4 sd = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
+            k.mn[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
+            k.sd[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
+            k.b0[i] = *reinterpret_cast<const f32x4*>(bias0 + ch0 + 16 * i);
+            k.b1[i] = bias1 ? *reinterpret_cast<const f32x4*>(bias1 + ch0 + 16 * i) : k.b0[i];
+        }
+        return k;
+    };
+    auto adain_act = [&](f32x4 (&v)[2][NF], const Cnd& k) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[i][f][r] = act_f(v[i][f][r] * sd[r] + mn[r], act);
+                for (int r = 0; r < 4; ++r) v[i][f][r] = act_f(v[i][f][r] * k.sd[i][r] + k.mn[i][r], act);
         }
     };
     auto put_stash = [&](const f32x4 (&v)[2][NF], int q, int half, int nfq, const f32x4 (&is)[2])
@@ -240,18 +241,22 @@ __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
         zero_acc(acc);
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(16 * f + c, Ti - 1);
+        // (prefetched on the standard shape only: the generic shapes' runtime fragment counts
+        // leave no registers for it)
+        Cnd k1;
+        if constexpr (STD) k1 = cnd_load(2 * l, A.w.b_c1[l], nullptr);
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c1(l), op_c2(l, 0), HB, rb);
+        if constexpr (!STD) k1 = cnd_load(2 * l, A.w.b_c1[l], nullptr);
         {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_c1[l] + ch0 + 16 * i);
 #pragma unroll
-                for (int f = 0; f < NF; ++f) acc[i][f] += bi;
+                for (int f = 0; f < NF; ++f) acc[i][f] += k1.b0[i];
             }
             f32x4 is[2];
             inorm_rows(acc, nfi, Ti, is);
             put_stash(acc, 2 * l, 0, nfq, is);
-            adain_act(acc, 2 * l);
+            adain_act(acc, k1);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -262,19 +267,24 @@ __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
         }
         __syncthreads();
         const AOp nxt = l + 1 < nblk ? op_c1(l + 1) : op_out();
+        Cnd k2;
+        auto k2_load = [&]() __attribute__((always_inline)) {
+            k2 = cnd_load(2 * l + 1, A.w.b_c2[l][0], up == 2 ? A.w.b_c2[l][1] : nullptr);
+        };
+        if constexpr (STD) k2_load();
         if (up == 1) {
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c2(l, 0), nxt, YB, rb);
+            if constexpr (!STD) k2_load();
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_c2[l][0] + ch0 + 16 * i);
 #pragma unroll
-                for (int f = 0; f < NF; ++f) acc[i][f] += bi;
+                for (int f = 0; f < NF; ++f) acc[i][f] += k2.b0[i];
             }
             f32x4 is[2];
             inorm_rows(acc, nfi, Ti, is);
             put_stash(acc, 2 * l + 1, 0, nfq, is);
-            adain_act(acc, 2 * l + 1);
+            adain_act(acc, k2);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -290,22 +300,21 @@ __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
             zero_acc(a1);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c2(l, 0), op_c2(l, 1), YB, rb);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(a1, nfi, ring, op_c2(l, 1), nxt, YB, rb);
+            if constexpr (!STD) k2_load();
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const f32x4 b0 = *reinterpret_cast<const f32x4*>(A.w.b_c2[l][0] + ch0 + 16 * i);
-                const f32x4 b1 = *reinterpret_cast<const f32x4*>(A.w.b_c2[l][1] + ch0 + 16 * i);
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
-                    acc[i][f] += b0;
-                    a1[i][f] += b1;
+                    acc[i][f] += k2.b0[i];
+                    a1[i][f] += k2.b1[i];
                 }
             }
             f32x4 is[2];
             inorm_rows2(acc, a1, nfi, Ti, is);
             put_stash(acc, 2 * l + 1, 0, nfq, is);
             put_stash(a1, 2 * l + 1, 1, nfq, is);
-            adain_act(acc, 2 * l + 1);
-            adain_act(a1, 2 * l + 1);
+            adain_act(acc, k2);
+            adain_act(a1, k2);
             // residual: y + upsample(h) -- frame 2t+s takes h[t] (lane-local per half)
             const int To = 2 * Ti;
 #pragma unroll
@@ -490,6 +499,43 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
     ring_fill(ring, op_outT());
     int rb[NF];
 
+    // what the AdaIN / IN backward of IN layer q reads from memory -- the conditions, 1/std and
+    // the stashed normalised activations (H halves x nfq fragments) -- loaded one GEMM ahead of
+    // its use (at its use, every layer paid an HBM round trip)
+    using SW = std::conditional_t<PREC == PREC_F32, f32x4, u32x2>;
+    struct AdnIn {
+        f32x4 mn[2], sd[2], is[2];
+        SW y[2][8][2];   // [tile][fragment][half]
+    };
+    auto adn_load = [&](int q, int H, int T) __attribute__((always_inline)) {
+        AdnIn k;
+        const int nfq = (T + 15) >> 4;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            k.mn[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
+            k.sd[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
+            k.is[i] = *reinterpret_cast<const f32x4*>(A.invstd + ((size_t)b * 2 * nblk + q) * 128 + ch0 + 16 * i);
+#pragma unroll
+            for (int f = 0; f < 8; ++f)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (f < nfq && h < H) k.y[i][f][h] = reinterpret_cast<const SW*>(A.stash)[dz_slot(A, b, q, h, nfq, f, i, w, 4)];
+        }
+        return k;
+    };
+    auto unpack = [&](const SW& v) __attribute__((always_inline)) {
+        if constexpr (PREC == PREC_F32) {
+            return v;
+        } else {   // bf16 -> f32 is exact: the bf16 bits in the high half
+            return f32x4{__builtin_bit_cast(float, v[0] << 16), __builtin_bit_cast(float, v[0] & 0xffff0000u),
+                         __builtin_bit_cast(float, v[1] << 16), __builtin_bit_cast(float, v[1] & 0xffff0000u)};
+        }
+    };
+    // (one GEMM ahead on the standard shape; the generic shapes' runtime fragment counts leave
+    // no registers for it: they load at the use)
+    AdnIn pf;
+    if constexpr (STD) pf = adn_load(2 * nblk - 1, StdDec::up(StdDec::NBLK - 1), StdDec::Tl(StdDec::NBLK - 1));
+
     // g(h_N) = out_conv^T g_out
     f32x4 gh[2][NF];
     zero_acc(gh);
@@ -510,20 +556,18 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
     //   d/dmean = sum g_z,  d/dstd = sum g_z yhat          -> g_cond[q]
     //   d/dx = invstd (g_y - mean(g_y) - yhat mean(g_y yhat)),  g_y = g_z std
     //        = invstd std (g_z - (sum g_z)/n - yhat (sum g_z yhat)/n)     (n = H*T)
-    auto adain_in_bwd = [&](f32x4 (&g0)[2][NF], f32x4 (&g1)[2][NF], int H, int q, int T, int nfq)
+    auto adain_in_bwd = [&](f32x4 (&g0)[2][NF], f32x4 (&g1)[2][NF], int H, int q, int T, int nfq, const AdnIn& K)
                             __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const f32x4 mn = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
-            const f32x4 sd = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
-            const f32x4 is = *reinterpret_cast<const f32x4*>(A.invstd + ((size_t)b * 2 * nblk + q) * 128 + ch0 + 16 * i);
+            const f32x4 mn = K.mn[i], sd = K.sd[i], is = K.is[i];
             f32x4 yh0[NF], yh1[NF];
             f32x4 gm = {0.f, 0.f, 0.f, 0.f}, gs = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 if (f >= nfq) continue;
                 const bool in = 16 * f + c < T;
-                yh0[f] = dz_stash_get<PREC>(A, b, q, 0, nfq, f, i, w);
+                yh0[f] = unpack(K.y[i][f < 8 ? f : 7][0]);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float z = g0[i][f][r] * act_d(yh0[f][r] * sd[r] + mn[r], act);
@@ -534,7 +578,7 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
                     }
                 }
                 if (H == 2) {
-                    yh1[f] = dz_stash_get<PREC>(A, b, q, 1, nfq, f, i, w);
+                    yh1[f] = unpack(K.y[i][f < 8 ? f : 7][1]);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float z = g1[i][f][r] * act_d(yh1[f][r] * sd[r] + mn[r], act);
@@ -611,7 +655,8 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
                     if (f < nfq) g0[i][f] = gh[i][f];
         }
         // conv2 branch: act, AdaIN(2l+1), IN backward -> dY images (half 0: GB, half 1: GB2)
-        adain_in_bwd(g0, g1, up, 2 * l + 1, Ti, nfq);
+        if constexpr (!STD) pf = adn_load(2 * l + 1, up, Ti);
+        adain_in_bwd(g0, g1, up, 2 * l + 1, Ti, nfq, pf);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -636,6 +681,7 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
         f32x4 acc[2][NF];
         zero_acc(acc);
         const AOp after = l > 0 ? op_c1T(l) : op_c2T(l, 0);
+        if constexpr (STD) pf = adn_load(2 * l, 1, Ti);   // the conv1 branch's, under the conv2^T GEMM
         if (up == 2) {
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l, 0), op_c2T(l, 1), GB, rb);
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l, 1), after, GB2, rb);
@@ -643,10 +689,11 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l, 0), after, GB, rb);
         }
         fold_edges(acc, Ti, P, FSCR);   // (barrier: GB / GB2 are free afterwards)
+        if constexpr (!STD) pf = adn_load(2 * l, 1, Ti);
         // conv1 branch: act, AdaIN(2l), IN backward; then conv1^T into the residual
         // (the first block's conv1 input is the in_conv output: mu is constant, stop)
         if (l > 0) {
-            adain_in_bwd(acc, g1, 1, 2 * l, Ti, nfq);
+            adain_in_bwd(acc, g1, 1, 2 * l, Ti, nfq, pf);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -655,6 +702,8 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
                     if (f < nfq && t < Ti) st4<PREC>(GB + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, acc[i][f]);
                 }
             __syncthreads();
+            // the next block's conv2 branch, under this conv1^T GEMM
+            if constexpr (STD) pf = adn_load(2 * (l - 1) + 1, StdDec::up(l - 1), StdDec::Tl(l - 1));
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c1T(l), op_c2T(l - 1, 0), GB, rb);
             fold_edges(acc, Ti, P, FSCR);
@@ -664,7 +713,7 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
                 for (int f = 0; f < NF; ++f)
                     if (f < nfq) gh[i][f] += acc[i][f];
         } else {
-            adain_in_bwd(acc, g1, 1, 0, Ti, nfq);   // g_cond[0] only
+            adain_in_bwd(acc, g1, 1, 0, Ti, nfq, pf);   // g_cond[0] only
         }
     };
     if constexpr (STD != 0) {
