@@ -766,7 +766,8 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         m1.load(mwords(nb + 1 + 2 * l));
         fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l), op_c1T(l), GB, rb);
         FZ_PH();
-        fold_edges(acc, Ti, P, FSCR);
+        // wave-local fold: GB2 (written next) was last read before this block's first barrier
+        fold_edges<false>(acc, Ti, P, FSCR);
         FZ_PH();
         {   // * act'(y1_l) -> GB2 (stride 1)
 #pragma unroll
@@ -789,7 +790,8 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         mnext.load(mwords(l > 0 ? nb + 2 + 2 * (l - 1) : nb));   // next block's conv2, or h0
         fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c1T(l), l > 0 ? op_c2T(l - 1) : op_c1T(l), GB2, rb);
         FZ_PH();
-        fold_edges(acc, Ti, P, FSCR);
+        // wave-local fold: GB (written next) was last read before the act' barrier above
+        fold_edges<false>(acc, Ti, P, FSCR);
         if (s == 2) {
             // g_h[t] += g_{l+1}[t/2] / cnt(t/2) (torch avg_pool backward: grad / divide_factor);
             // decreasing f keeps the in-place update safe (frag f reads frag f/2)

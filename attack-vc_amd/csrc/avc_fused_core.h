@@ -379,8 +379,10 @@ __device__ __forceinline__ int vpos(int n, int Tin, int E) {
 // interior frame -v (left) or 2(Tin-1)-v (right)   (F.pad mode="reflect", models.py:23-29).
 // Edge column e (n = Tin + e) is staged through this wave's LDS scratch [MT*16 ch][8]
 // and pulled by its target lane: fragment indices stay compile-time (no dynamic
-// register indexing).  Called by all waves at the same point (contains a barrier).
-template <int MT, int NF>
+// register indexing).  The scratch is the wave's own, so the hand-off needs no workgroup
+// barrier (a wave's LDS accesses execute in order); BAR = true keeps one for callers that
+// use it to free other LDS (every wave must then call it at the same point).
+template <bool BAR = true, int MT, int NF>
 __device__ __forceinline__ void fold_edges(f32x4 (&acc)[MT][NF], int Tin, int E, float* scr) {
     const int lane = threadIdx.x & 63, c = lane & 15, kq = lane >> 4;
 #pragma unroll
@@ -393,7 +395,8 @@ __device__ __forceinline__ void fold_edges(f32x4 (&acc)[MT][NF], int Tin, int E,
                 for (int r = 0; r < 4; ++r) scr[(16 * i + 4 * kq + r) * 8 + e] = acc[i][f][r];
         }
     }
-    __syncthreads();
+    if constexpr (BAR) __syncthreads();
+    else asm volatile("" ::: "memory");
 #pragma unroll
     for (int g = 0; g < NF; ++g) {
         const int t = 16 * g + c;
