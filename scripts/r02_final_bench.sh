@@ -13,6 +13,7 @@ run() {   # name timeout args...
 }
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; tail -20 $O/smoke.log; exit 1; }
 echo smoke ok
+[ "${ONLY_EMB:-0}" = 1 ] && { run bench_emb 600 --steps 2 --warmup 1; echo ALL_OK; exit 0; }
 run bench_emb 600 --steps 2 --warmup 1
 run bench_e2e 600 --attack e2e --steps 1 --warmup 1 --no-fp32-compare
 run bench_fb 600 --attack fb --steps 1 --warmup 1 --no-fp32-compare
