@@ -912,7 +912,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                     st4<PREC>(GBK + (ZPB + 16 * f + c) * RS + (ch0 + 16 * i) * ESZ, v);
                 }
             }
-            __syncthreads();
+            // wave-local hand-off (as in se_bwd_fused): the bank^T below reads only this wave's
+            // g(b_k) channels, and GP is read-only here -- program order, no workgroup barrier
+            asm volatile("" ::: "memory");
             // bank_k^T over this wave's channel quarter: rows u = v + pl - j of g(b_k)
 #pragma unroll
             for (int f = 0; f < LZ_CHF; ++f) {
@@ -925,7 +927,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             } else {
                 fz_gemm<PREC, 5, LZ_CHF, FZ_C, -1>(accx, IC<CHF>{}, ring5, op_bankT(kb), nxt, GBK, rb);
             }
-            __syncthreads();
+            asm volatile("" ::: "memory");   // (the next gate rewrites this wave's slice: in order)
         };
         for (int kb = 0; kb < nb; ++kb) bank_step(kb);
         if (!chk.last) {   // ring5 now holds op_bankT(nb-1) prefetches; the next chunk starts at in_x^T
@@ -949,8 +951,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             __syncthreads();
         }
         // owned interior columns: t = n - 4 in [0, T).  UB elements per thread per batch, all
-        // their state loads issued before any arithmetic (one memory round trip per batch)
-        constexpr int UB = 4;
+        // their state loads issued before any arithmetic (one memory round trip per batch; 20:
+        // two round trips per 128-column chunk instead of ten)
+        constexpr int UB = 20;
         for (int i0 = 0; i0 < FZ_CIN * CH; i0 += 256 * UB) {
             size_t qv[UB];
             bool ok[UB];
