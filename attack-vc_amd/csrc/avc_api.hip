@@ -1745,6 +1745,35 @@ static int stage_call_consts(avc_ctx* ctx, int n_iters, const float scal[4], dou
     return 0;
 }
 
+// Graph replay of an iteration plan: GRAPH_ITERS iterations are captured into ONE graph (the Adam step
+// counter lives in HBM, so consecutive iterations are identical launches) -- a graph launch
+// per iteration left ~9 us between the backward's end and the next forward's start (kernel
+// trace), against none between the kernels inside a graph.  The n_iters % GRAPH_ITERS tail runs as
+// plain launches.
+constexpr int GRAPH_ITERS = 10;
+static int graph_replay(avc_ctx* ctx, Plan& iter, hipGraphExec_t& graph, int n_iters) {
+    const int nfull = n_iters / GRAPH_ITERS;
+    if (nfull > 0 && !graph) {
+        hipGraph_t g;
+        HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        int rc = 0;
+        for (int it = 0; it < GRAPH_ITERS && !rc; ++it) rc = run_plan(ctx, iter, false);
+        hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        if (rc) return 1;
+        if (e != hipSuccess) return fail("graph capture: %s", hipGetErrorString(e));
+        e = hipGraphInstantiate(&graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (e != hipSuccess) {
+            graph = nullptr;
+            return fail("graph instantiate: %s", hipGetErrorString(e));
+        }
+    }
+    for (int it = 0; it < nfull; ++it) HIPCHK(hipGraphLaunch(graph, ctx->stream));
+    for (int it = nfull * GRAPH_ITERS; it < n_iters; ++it)
+        if (run_plan(ctx, iter, false)) return 1;
+    return 0;
+}
+
 // emb attack; the target embedding is SE(adv_tgt) at T frames (adv_tgt given) or the caller's
 // tgt_emb [B][c_out] (adv_tgt of another length, embedded beforehand by avc_se_forward)
 static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* tgt_emb,
@@ -1817,21 +1846,7 @@ static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_t
         hipEventDestroy(a);
         hipEventDestroy(b);
     } else if (o.use_graph && n_iters > 0 && !(getenv("AVC_NO_GRAPH") && getenv("AVC_NO_GRAPH")[0] == '1')) {
-        if (!graph) {
-            hipGraph_t g;
-            HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-            int rc = run_plan(ctx, iter, false);
-            hipError_t e = hipStreamEndCapture(ctx->stream, &g);
-            if (rc) return 1;
-            if (e != hipSuccess) return fail("graph capture: %s", hipGetErrorString(e));
-            e = hipGraphInstantiate(&graph, g, nullptr, nullptr, 0);
-            hipGraphDestroy(g);
-            if (e != hipSuccess) {
-                graph = nullptr;
-                return fail("graph instantiate: %s", hipGetErrorString(e));
-            }
-        }
-        for (int it = 0; it < n_iters; ++it) HIPCHK(hipGraphLaunch(graph, ctx->stream));
+        if (graph_replay(ctx, iter, graph, n_iters)) return 1;
     } else {
         for (int it = 0; it < n_iters; ++it)
             if (run_plan(ctx, iter, false)) return 1;
