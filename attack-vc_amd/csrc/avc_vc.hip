@@ -851,9 +851,13 @@ __global__ void __launch_bounds__(256) dense_mfma(DenseArgs D) {
         const int bb = b0 + 16 * j + r16;
         if (bb >= D.B) continue;
         const f32x4 y = (j ? acc1 : acc0) + bi;
+        if ((D.M & 3) == 0 && m + 3 < D.M) {   // 4 consecutive rows: one 16-byte store
+            *reinterpret_cast<f32x4*>(Y + (size_t)bb * D.M + m) = y;
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (m + r < D.M) Y[(size_t)bb * D.M + m + r] = y[r];
+            for (int r = 0; r < 4; ++r)
+                if (m + r < D.M) Y[(size_t)bb * D.M + m + r] = y[r];
+        }
     }
 }
 
