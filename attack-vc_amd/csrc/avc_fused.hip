@@ -91,18 +91,20 @@ __device__ __forceinline__ int hpos(int k) { return ((k >> 1) & 3) * 36 + 2 * (k
 // sum_k W[m][k] X[k] over this lane's K slice, then over the row's 4 slices (DPP)
 __device__ __forceinline__ float head_dot(const HW16& hw, const float* X, int q) {
 #pragma clang fp contract(off)
-    float acc = 0.f, acc2 = 0.f;   // even / odd k of each pair (se_head_v's order)
+    // the even / odd k of each pair accumulate separately (se_head_v's order) -- as the two
+    // lanes of one packed fma (v_pk_fma_f32: each lane an IEEE fma, so bitwise the same sums)
+    f32x2 acc2v = {0.f, 0.f};
     const f32x4* X4 = reinterpret_cast<const f32x4*>(X + q * 36);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const f32x4 x = X4[e];     // pairs i = 2e (x0, x1) and i = 2e + 1 (x2, x3), k = 8i + 2q
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            acc = fmaf(hw16_w(hw, e, 2 * h), x[2 * h], acc);
-            acc2 = fmaf(hw16_w(hw, e, 2 * h + 1), x[2 * h + 1], acc2);
+            const f32x2 wv = {hw16_w(hw, e, 2 * h), hw16_w(hw, e, 2 * h + 1)};
+            acc2v = __builtin_elementwise_fma(wv, f32x2{x[2 * h], x[2 * h + 1]}, acc2v);
         }
     }
-    acc = acc + acc2;
+    float acc = acc2v[0] + acc2v[1];
     acc += dpp_mov<0xB1>(acc);
     acc += dpp_mov<0x4E>(acc);
     return acc;
