@@ -1750,7 +1750,7 @@ static int stage_call_consts(avc_ctx* ctx, int n_iters, const float scal[4], dou
 // per iteration left ~9 us between the backward's end and the next forward's start (kernel
 // trace), against none between the kernels inside a graph.  The n_iters % GRAPH_ITERS tail runs as
 // plain launches.
-constexpr int GRAPH_ITERS = 10;
+constexpr int GRAPH_ITERS = 50;
 static int graph_replay(avc_ctx* ctx, Plan& iter, hipGraphExec_t& graph, int n_iters) {
     const int nfull = n_iters / GRAPH_ITERS;
     if (nfull > 0 && !graph) {

@@ -132,7 +132,7 @@ def test_graph_and_eager_agree(gpu, golden):
     z = golden("small_T32")
     m = model_from_fixture(z).to(gpu)
     ctx = avc_native.context_for(m.speaker_encoder, gpu)
-    args = (_dev(z["vc_tgt"]), _dev(z["adv_tgt"]), _dev(z["emb_ptb0"]), 0.1, 25)
+    args = (_dev(z["vc_tgt"]), _dev(z["adv_tgt"]), _dev(z["emb_ptb0"]), 0.1, 55)   # one 50-iteration graph + 5
     a, _, _ = ctx.emb_attack(*args, use_graph=True)
     b, _, _ = ctx.emb_attack(*args, use_graph=False)
     assert torch.equal(a, b)

@@ -142,8 +142,8 @@ def test_vc_small_config_rejected(golden):
 
 @pytest.mark.parametrize("kind", ["emb", "e2e", "fb"])
 def test_graph_tail_matches_eager(full, kind):
-    """The attack loop replays a captured graph of ten iterations plus plain launches for the
-    n_iters % 10 tail (csrc/avc_api.hip graph_replay): at n = 23 (two graphs + three launches),
+    """The attack loop replays a captured graph of 50 iterations plus plain launches for the
+    n_iters % 50 tail (csrc/avc_api.hip graph_replay): at n = 103 (two graphs + three launches),
     bf16, the adversarial output and the whole per-iteration loss history equal the eager
     (one launch per kernel) run bitwise."""
     from avc_native import context_for, vc_context_for
@@ -152,12 +152,12 @@ def test_graph_tail_matches_eager(full, kind):
     src, vc, at, p0 = (torch.randn(2, 80, 128, generator=g).to(DEV) for _ in range(4))
     if kind == "emb":
         ctx = context_for(m.speaker_encoder, DEV)
-        run = lambda gr: ctx.emb_attack(vc, at, p0, 0.1, 23, precision="bf16", use_graph=gr, want_losses=True)
+        run = lambda gr: ctx.emb_attack(vc, at, p0, 0.1, 103, precision="bf16", use_graph=gr, want_losses=True)
     else:
         ctx = vc_context_for(m, DEV)
-        run = lambda gr: ctx.vc_attack(kind, src, vc, at, p0, 0.1, 23, precision="bf16", use_graph=gr,
+        run = lambda gr: ctx.vc_attack(kind, src, vc, at, p0, 0.1, 103, precision="bf16", use_graph=gr,
                                        want_losses=True)
     a, la, _ = run(True)
     b, lb, _ = run(False)
     assert torch.equal(a, b)
-    assert la.shape[0] == 23 and torch.equal(la, lb)
+    assert la.shape[0] == 103 and torch.equal(la, lb)
