@@ -13,11 +13,15 @@ this module restates the published algorithms of librosa 0.8.1 (the release
 of the reference's era): `filters.mel` (Slaney mel scale, Slaney area
 normalisation), `stft` / `istft` (centered frames, periodic Hann window padded
 to n_fft, window-sum-square normalisation), `effects.trim` (frame RMS in dB
-against the peak).  PARITY UNPINNED against librosa itself: there is no
-librosa output in the reference to pin it to.  What is pinned: the restated
-transforms satisfy the properties the reference relies on (perfect STFT ->
-ISTFT reconstruction, Slaney filter areas, the reference's own composition of
-them in file2mel / mel2wav / griffin_lim), tested in tests/test_dsp_oracle.py.
+against the peak).
+Pinned against scipy 1.15 (importable here; the reference calls scipy.signal
+itself, data_utils.py:163): the Hann window (`scipy.signal.get_window`), the
+STFT / ISTFT (`scipy.signal.stft` / `istft` with the even (= reflect) boundary),
+the de-emphasis (`scipy.signal.lfilter`) and the reference's Griffin-Lim
+composition on those transforms -- to 1e-12 relative (tests/test_dsp_oracle.py).
+PARITY UNPINNED for the two pieces only librosa defines: the Slaney mel filter
+bank and `effects.trim` (no librosa output exists in the reference); they are
+checked by properties (filter areas, trim bounds).
 
 Computation is float64 (numpy's pocketfft computes in double, as librosa's
 calls did).

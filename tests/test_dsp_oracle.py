@@ -205,3 +205,68 @@ def test_attack_cli_flags_match_reference():
     assert (a.vc_src, a.eps, a.n_iters, a.attack_type) == ("s", 0.05, 10, "fb")
     with pytest.raises(SystemExit):
         attack.build_parser().parse_args(["m", "t", "a", "o", "--attack_type", "xx"])
+
+
+# ---- oracle primitives pinned against scipy (the reference's own DSP library besides librosa:
+# data_utils.py:163 calls scipy.signal.lfilter; librosa 0.8's get_window / stft / istft are
+# scipy.signal.get_window + a centered reflect-padded framing that scipy.signal.stft /
+# istft(boundary='even' / True) reproduce).  librosa itself is absent: the mel filter bank and
+# trim stay restated (parity of those two unpinned), everything else below is pinned here.
+
+def _scipy_stft(y, n_fft, hop, win):
+    import scipy.signal as ss
+    w = mel_dsp.stft_window(n_fft, win)
+    _, _, Z = ss.stft(y, fs=1.0, window=w, nperseg=n_fft, noverlap=n_fft - hop, nfft=n_fft, detrend=False,
+                      return_onesided=True, boundary="even", padded=False, scaling="spectrum")
+    return Z * w.sum()            # scaling="spectrum" divides by sum(window); librosa does not
+
+
+def _scipy_istft(S, n_fft, hop, win):
+    import scipy.signal as ss
+    w = mel_dsp.stft_window(n_fft, win)
+    _, y = ss.istft(S / w.sum(), fs=1.0, window=w, nperseg=n_fft, noverlap=n_fft - hop, nfft=n_fft,
+                    input_onesided=True, boundary=True, scaling="spectrum")
+    return y
+
+
+@pytest.mark.parametrize("win", [1200, 2048, 801])
+def test_hann_window_is_scipy(win):
+    import scipy.signal as ss
+    np.testing.assert_allclose(mel_dsp.hann_periodic(win), ss.get_window("hann", win, fftbins=True),
+                               rtol=0, atol=1e-15)
+
+
+def test_deemphasis_is_scipy_lfilter():
+    """data_utils.py:163: signal.lfilter([1], [1, -preemph], wav)."""
+    import scipy.signal as ss
+    x = np.random.default_rng(3).standard_normal(20000)
+    for a in (0.97, 0.5):
+        np.testing.assert_allclose(mel_dsp.deemphasis(x, a), ss.lfilter([1], [1, -a], x), rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("n_fft,hop,win,n", [(2048, 300, 1200, 16000), (512, 128, 512, 4000), (1024, 256, 600, 7001)])
+def test_stft_istft_are_scipy(n_fft, hop, win, n):
+    y = np.random.default_rng(n).standard_normal(n)
+    S = mel_dsp.stft(y, n_fft, hop, win)
+    Z = _scipy_stft(y, n_fft, hop, win)
+    assert S.shape == Z.shape
+    assert np.abs(S - Z).max() <= 1e-12 * np.abs(S).max()
+    yo = mel_dsp.istft(S, hop, win)
+    ys = _scipy_istft(S, n_fft, hop, win)
+    assert np.abs(yo - ys[:len(yo)]).max() <= 1e-12 * np.abs(yo).max()
+
+
+def test_griffin_lim_composition_on_scipy():
+    """The reference's griffin_lim (data_utils.py:168-197) composed of scipy's transforms equals
+    the oracle's (3 iterations of a random magnitude)."""
+    n_fft, hop, win = 512, 128, 400
+    mag = np.abs(np.random.default_rng(5).standard_normal((n_fft // 2 + 1, 40)))
+    X = mag.astype(np.complex128)
+    for _ in range(3):
+        xt = _scipy_istft(X, n_fft, hop, win)[:hop * (mag.shape[1] - 1)]
+        est = _scipy_stft(xt, n_fft, hop, win)
+        X = mag * (est / np.maximum(1e-8, np.abs(est)))
+    ref = np.real(_scipy_istft(X, n_fft, hop, win))[:hop * (mag.shape[1] - 1)]
+    out = mel_dsp.griffin_lim(mag, hop, win, n_fft, n_iter=3)
+    assert out.shape == ref.shape
+    np.testing.assert_allclose(out, ref, rtol=0, atol=1e-10 * np.abs(ref).max())

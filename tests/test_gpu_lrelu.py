@@ -44,3 +44,46 @@ def test_lrelu_attacks(lrelu, kind):
         adv, info = fn(m, t["vc_src"], t["vc_tgt"], t["adv_tgt"], 0.1, 10, ptb0=t[f"{kind}_ptb0"], return_info=True)
     check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10)
     assert rel(info["grad0"].cpu().numpy(), z[f"{kind}_grad0"]) <= (TOL_GRAD_REL_VC if kind != "emb" else TOL_GRAD_REL)
+
+
+@pytest.mark.parametrize("T", [300, 200])
+def test_lrelu_long_engine_vs_oracle(lrelu, T):
+    """LeakyReLU(0.01) on the long engine (T > 128: csrc/avc_long.hip's epilogues and its act'
+    from the ballot words) vs the float64 oracle: SpeakerEncoder(x), the emb attack's grad0 /
+    10-iteration adv / losses, inference, and the e2e / fb iteration-0 gradients (normwise per
+    utterance, helpers.TOL_VC_GRAD_*).  vc_src / adv_tgt of other lengths on the way."""
+    from helpers import TOL_VC_GRAD_L2_MAX, TOL_VC_GRAD_L2_MEDIAN, cfg_of
+    from oracle import adain_vc as oracle
+    z, m = lrelu
+    ctx = avc_native.context_for(m.speaker_encoder, DEV)
+    assert ctx.engine_for(T) == "long"
+    cfg = cfg_of(z)
+    assert cfg["SpeakerEncoder"]["act"] == "lrelu"
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    w64 = oracle.Weights(sd, dtype=np.float64)
+    g = torch.Generator().manual_seed(700 + T)
+    vc, p0 = (torch.randn(2, 80, T, generator=g) for _ in range(2))
+    at = torch.randn(2, 80, T - 21, generator=g)
+    src = torch.randn(2, 80, T + 11, generator=g)
+    d = lambda t: t.to(DEV)
+    f64 = lambda t: t.double().numpy()
+    e = ctx.se_forward(d(vc)).cpu().numpy()
+    eo, _ = oracle.se_forward(w64, cfg["SpeakerEncoder"], f64(vc))
+    assert rel(e, eo) <= TOL_SE_REL, rel(e, eo)
+    adv, info = attack_utils.emb_attack(m, d(vc), d(at), 0.1, 10, ptb0=d(p0), return_info=True)
+    rec = {}
+    ref = oracle.emb_attack(w64, cfg, f64(vc), f64(at), 0.1, 10, f64(p0), record=rec)
+    assert rel(info["grad0"].cpu().numpy(), rec["grad0"]) <= TOL_GRAD_REL
+    check_adv(adv.detach().cpu().numpy(), ref, 10)
+    np.testing.assert_allclose(info["losses"].cpu().numpy().T, rec["losses"], rtol=2e-4, atol=1e-9)
+    out = m.inference(d(src), d(vc)).cpu().numpy()
+    ro = oracle.inference(w64, cfg, f64(src), f64(vc))
+    assert out.shape == ro.shape and rel(out, ro) <= 1e-4, rel(out, ro)
+    for kind in ("e2e", "fb"):
+        rec = {}
+        getattr(oracle, f"{kind}_attack")(w64, cfg, f64(src), f64(vc), f64(at), 0.1, 1, f64(p0), record=rec)
+        fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
+        _, info = fn(m, d(src), d(vc), d(at), 0.1, 1, ptb0=d(p0), return_info=True)
+        gg = info["grad0"].cpu().numpy().astype(np.float64)
+        err = [float(np.linalg.norm(gg[u] - rec["grad0"][u]) / np.linalg.norm(rec["grad0"][u])) for u in range(2)]
+        assert max(err) <= TOL_VC_GRAD_L2_MAX and float(np.median(err)) <= 5 * TOL_VC_GRAD_L2_MEDIAN, (kind, err)

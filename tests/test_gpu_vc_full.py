@@ -1,0 +1,83 @@
+"""GPU parity of the e2e / feedback attacks at the bench horizon and size:
+
+  * the reference's own 100-iteration e2e / fb outputs (tests/golden/full_T128_n100.npz, made
+    by attack_utils.e2e_attack / fb_attack on CPU from full_T128.npz's inputs) -- adv at the
+    SURVEY 8(c) fp32 tolerances for n = 100 (max 1e-3, mean 1e-6), grad0 and the whole loss
+    history at rtol 2e-4;
+  * configs[2] / configs[3]'s own size, B = 256 and T = 128 (the bench workload): determinism,
+    the perturbation bound |adv - vc| <= eps, the per-utterance loss decreasing, and two utterances of
+    the batch spot-checked against the float64 oracle over 50 iterations -- in fp32, then the
+    same properties in the bench's bf16 mode plus the SURVEY 8(c) bf16 adv bound.
+
+Reference: /root/reference/attack_utils.py:7-48 (e2e), 89-130 (fb)."""
+import numpy as np
+import pytest
+import torch
+
+import attack_utils
+from helpers import TOL_GRAD_REL_VC, cfg_of, check_adv, model_from_fixture, rel
+from oracle import adain_vc as oracle
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+FN = {"e2e": attack_utils.e2e_attack, "fb": attack_utils.fb_attack}
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.fixture(scope="module")
+def full(golden):
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    z = golden("full_T128")
+    return z, model_from_fixture(z).to(DEV)
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_vc_attack_golden_n100(full, golden, kind):
+    """attack_utils.{e2e,fb}_attack after 100 iterations (the reference's own fp32 run)."""
+    z, m = full
+    zn = golden("full_T128_n100")
+    adv, info = FN[kind](m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 100,
+                         ptb0=_dev(zn[f"{kind}_ptb0"]), return_info=True)
+    check_adv(adv.detach().cpu().numpy(), zn[f"{kind}_adv_n100"], 100)
+    assert rel(info["grad0"].cpu().numpy(), zn[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
+    np.testing.assert_allclose(info["losses"].cpu().numpy().T, zn[f"{kind}_losses_n100"], rtol=2e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_vc_full_size_properties(full, kind):
+    """B = 256, T = 128, n = 50 (the bench's shape): fp32 then bf16."""
+    z, m = full
+    g = torch.Generator().manual_seed(31 if kind == "e2e" else 32)
+    B, T, n = 256, 128, 50
+    src, vc, at = (torch.randn(B, 80, T, generator=g).to(DEV) for _ in range(3))
+    p0 = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(123)).to(DEV)
+    fn = FN[kind]
+    a, info = fn(m, src, vc, at, 0.1, n, ptb0=p0, return_info=True)
+    a = a.detach()
+    b = fn(m, src, vc, at, 0.1, n, ptb0=p0).detach()
+    assert torch.equal(a, b)
+    assert float((a - vc).abs().max()) <= 0.1 + 1e-6
+    L = info["losses"].cpu().numpy()                 # [n, B]
+    assert np.all(L[-1] < L[0]), int(np.sum(L[-1] >= L[0]))
+    # two utterances of the batch vs the float64 oracle (its fp32 restatement drifts ~1e-5 max
+    # / 1e-7 mean from it over these 50 iterations; bound: SURVEY 8(c)'s n = 100 fp32 tolerances)
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    w64 = oracle.Weights(sd, dtype=np.float64)
+    idx = [0, B - 1]
+    f64 = [t[idx].cpu().numpy().astype(np.float64) for t in (src, vc, at, p0)]
+    ref = getattr(oracle, f"{kind}_attack")(w64, cfg_of(z), *f64[:3], 0.1, n, f64[3])
+    d = np.abs(a[idx].cpu().numpy().astype(np.float64) - ref)
+    assert d.max() <= 1e-3 and d.mean() <= 1e-6, (d.max(), d.mean())
+    # the bench's precision: bf16 MFMA operands, fp32 accumulation and Adam state
+    a16, info16 = fn(m, src, vc, at, 0.1, n, ptb0=p0, precision="bf16", return_info=True)
+    a16 = a16.detach()
+    b16 = fn(m, src, vc, at, 0.1, n, ptb0=p0, precision="bf16").detach()
+    assert torch.equal(a16, b16)
+    assert float((a16 - vc).abs().max()) <= 0.1 + 1e-6
+    L16 = info16["losses"].cpu().numpy()
+    assert np.all(L16[-1] < L16[0]), int(np.sum(L16[-1] >= L16[0]))
+    assert float((a16 - a).abs().max()) <= 2e-2            # SURVEY 8(c) bf16 adv bound (n <= 100)

@@ -132,6 +132,22 @@ def test_vc_attacks(golden, name, kind):
     np.testing.assert_allclose(rec["losses"], z[f"{kind}_losses_n10"], rtol=1e-4, atol=1e-9)
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_vc_attacks_full_n100(golden, kind):
+    """The reference's 100-iteration e2e / fb runs (full_T128_n100.npz, inputs of full_T128.npz)
+    reproduced by the fp32 restatement: adv at SURVEY 8(c)'s n = 100 tolerances, grad0, losses."""
+    z = golden("full_T128")
+    zn = golden("full_T128_n100")
+    w = oracle_weights(model_from_fixture(z))
+    rec = {}
+    adv = getattr(oracle, f"{kind}_attack")(w, cfg_of(z), z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 100,
+                                            zn[f"{kind}_ptb0"], record=rec)
+    check_adv(adv, zn[f"{kind}_adv_n100"], 100)
+    assert rel(rec["grad0"], zn[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
+    np.testing.assert_allclose(rec["losses"], zn[f"{kind}_losses_n100"], rtol=2e-4, atol=1e-9)
+
+
 def test_decoder_backward_is_adjoint():
     """<d out, J d cond> == <J^T d out, d cond> for the numpy Decoder (finite differences
     in float64 on a tiny random decoder)."""
