@@ -80,6 +80,11 @@ SIGNATURES = [
                                            ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                            ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_header_optimize_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_float,
+                                                 ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                                 ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     ("avc_vc_weight_count", ctypes.c_size_t, [ctypes.POINTER(VCCfg)]),
     ("avc_attach_vc", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(VCCfg), ctypes.c_void_p, ctypes.c_size_t]),
     ("avc_vc_out_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -136,6 +141,8 @@ SIGNATURES = [
     ("avc_profile_kernel", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_double)]),
+    ("avc_ws_stats", ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int64)] * 5),
+    ("avc_set_ws_cache", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_last_error", ctypes.c_char_p, []),
     ("avc_version", ctypes.c_char_p, []),
 ]
@@ -237,24 +244,37 @@ class Context:
                        grad0.data_ptr() if grad0 is not None else None, UPDATE[update], float(pgd_step))
         return o, losses, grad0
 
+    def _tgt_emb(self, tgt_emb, B):
+        _require_gpu(tgt_emb)
+        if tuple(tgt_emb.shape) != (B, self.cfg["c_out"]):
+            raise RuntimeError(f"tgt_emb: expected [{B}, {self.cfg['c_out']}], got {tuple(tgt_emb.shape)}")
+        return tgt_emb.contiguous()
+
     def emb_attack(self, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
                    reduction="independent", use_graph=True, want_losses=False, want_grad0=False, update="adam",
-                   pgd_step=1e-3):
+                   pgd_step=1e-3, tgt_emb=None):
         """avc_emb_attack; an adv_tgt of another length than vc_tgt is embedded on its own first
-        (the reference embeds it separately, attack_utils.py:74-75) -> avc_emb_attack_emb."""
-        _require_gpu(vc_tgt, adv_tgt, ptb0)
-        vc_tgt, adv_tgt, ptb0 = vc_tgt.contiguous(), adv_tgt.contiguous(), ptb0.contiguous()
+        (the reference embeds it separately, attack_utils.py:74-75) -> avc_emb_attack_emb.
+        tgt_emb [B, c_out] (= SpeakerEncoder(adv_tgt), computed by the caller) replaces adv_tgt."""
+        _require_gpu(vc_tgt, ptb0)
+        vc_tgt, ptb0 = vc_tgt.contiguous(), ptb0.contiguous()
         c_in = self.cfg["c_in"]
         self._check_mel("vc_tgt", vc_tgt, c_in)
         B, C, T = vc_tgt.shape
-        self._check_mel("adv_tgt", adv_tgt, c_in, B)
+        if tgt_emb is None:
+            _require_gpu(adv_tgt)
+            adv_tgt = adv_tgt.contiguous()
+            self._check_mel("adv_tgt", adv_tgt, c_in, B)
         if ptb0.shape != vc_tgt.shape:
             raise RuntimeError(f"shape mismatch: vc_tgt {tuple(vc_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
         out = torch.empty_like(vc_tgt)
         o, losses, grad0 = self._opts(precision, reduction, use_graph, n_iters, vc_tgt, want_losses, want_grad0,
                                       update, pgd_step)
         stream = torch.cuda.current_stream(vc_tgt.device).cuda_stream
-        tgt_emb = self.se_forward(adv_tgt) if adv_tgt.shape != vc_tgt.shape else None
+        if tgt_emb is not None:
+            tgt_emb = self._tgt_emb(tgt_emb, B)
+        elif adv_tgt.shape != vc_tgt.shape:
+            tgt_emb = self.se_forward(adv_tgt)
         with self._lock:
             if tgt_emb is None:
                 _check(lib().avc_emb_attack(self.h, ctypes.c_void_p(vc_tgt.data_ptr()),
@@ -269,9 +289,12 @@ class Context:
         return out, losses, grad0
 
     def header_optimize(self, source, target, header, n_iters: int, epsilon=0.1, lambda_param=0.5, lr=1e-3,
-                        betas=(0.9, 0.999), adam_eps=1e-8, precision="fp32"):
+                        betas=(0.9, 0.999), adam_eps=1e-8, precision="fp32", adam_state=None):
         """avc_header_optimize (UniversalPerturbationHeader.optimize, header_model.py:25-68):
-        source / target [N, 80, T], header [80, T] -> (new header [80, T], losses [n_iters, N])."""
+        source / target [N, 80, T], header [80, T] -> (new header [80, T], losses [n_iters, N]).
+        adam_state = (exp_avg [80, T], exp_avg_sq [80, T], step) continues an optimiser: the two
+        moment tensors are updated in place and the caller advances its step by n_iters
+        (avc_header_optimize_state)."""
         _require_gpu(source, target, header)
         source, target = source.contiguous(), target.contiguous()
         c_in = self.cfg["c_in"]
@@ -287,12 +310,20 @@ class Context:
         hdr = header.detach().clone().contiguous()
         losses = torch.empty(max(int(n_iters), 1), N, device=source.device, dtype=torch.float32)
         stream = torch.cuda.current_stream(source.device).cuda_stream
+        m = v = None
+        step0 = 0
+        if adam_state is not None:
+            m, v, step0 = adam_state
+            _require_gpu(m, v)
+            if tuple(m.shape) != (c_in, T) or tuple(v.shape) != (c_in, T) or not (m.is_contiguous() and v.is_contiguous()):
+                raise RuntimeError(f"Adam state must be contiguous [{c_in}, {T}] tensors")
         with self._lock:
-            _check(lib().avc_header_optimize(self.h, ctypes.c_void_p(source.data_ptr()),
-                                             ctypes.c_void_p(target.data_ptr()), N, T, ctypes.c_void_p(hdr.data_ptr()),
-                                             float(epsilon), float(lambda_param), float(lr), float(betas[0]),
-                                             float(betas[1]), float(adam_eps), int(n_iters), PREC[precision],
-                                             ctypes.c_void_p(losses.data_ptr()), ctypes.c_void_p(stream)))
+            _check(lib().avc_header_optimize_state(
+                self.h, ctypes.c_void_p(source.data_ptr()), ctypes.c_void_p(target.data_ptr()), N, T,
+                ctypes.c_void_p(hdr.data_ptr()), float(epsilon), float(lambda_param), float(lr), float(betas[0]),
+                float(betas[1]), float(adam_eps), int(n_iters), PREC[precision], ctypes.c_void_p(losses.data_ptr()),
+                ctypes.c_void_p(m.data_ptr() if m is not None else 0), ctypes.c_void_p(v.data_ptr() if v is not None else 0),
+                int(step0), ctypes.c_void_p(stream)))
         return hdr, losses[:n_iters]
 
     # --- voice-conversion path (ContentEncoder + Decoder) ----------------------------
@@ -336,17 +367,21 @@ class Context:
 
     def vc_attack(self, kind: str, vc_src, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
                   reduction="independent", use_graph=True, want_losses=False, want_grad0=False, update="adam",
-                  pgd_step=1e-3):
+                  pgd_step=1e-3, tgt_emb=None):
         """kind "e2e" (avc_e2e_attack) or "fb" (avc_fb_attack).  vc_src, vc_tgt and adv_tgt may have
         different lengths (each is loaded from its own wav by attack.py:49-56): then adv_tgt is
-        embedded on its own and the *_attack_emb entry points run."""
-        _require_gpu(vc_src, vc_tgt, adv_tgt, ptb0)
-        vc_src, vc_tgt, adv_tgt, ptb0 = (t.contiguous() for t in (vc_src, vc_tgt, adv_tgt, ptb0))
+        embedded on its own and the *_attack_emb entry points run.  tgt_emb [B, c_out] (=
+        SpeakerEncoder(adv_tgt), computed by the caller) replaces adv_tgt."""
+        _require_gpu(vc_src, vc_tgt, ptb0)
+        vc_src, vc_tgt, ptb0 = (t.contiguous() for t in (vc_src, vc_tgt, ptb0))
         c_in = self.cfg["c_in"]
         self._check_mel("vc_tgt", vc_tgt, c_in)
         B, C, T = vc_tgt.shape
         self._check_mel("vc_src", vc_src, c_in, B)
-        self._check_mel("adv_tgt", adv_tgt, c_in, B)
+        if tgt_emb is None:
+            _require_gpu(adv_tgt)
+            adv_tgt = adv_tgt.contiguous()
+            self._check_mel("adv_tgt", adv_tgt, c_in, B)
         if ptb0.shape != vc_tgt.shape:
             raise RuntimeError(f"shape mismatch: vc_tgt {tuple(vc_tgt.shape)}, ptb0 {tuple(ptb0.shape)}")
         Ts = vc_src.shape[2]
@@ -354,8 +389,12 @@ class Context:
         o, losses, grad0 = self._opts(precision, reduction, use_graph, n_iters, vc_tgt, want_losses, want_grad0,
                                       update, pgd_step)
         stream = torch.cuda.current_stream(vc_tgt.device).cuda_stream
-        same = vc_src.shape == vc_tgt.shape == adv_tgt.shape
-        tgt_emb = None if same else self.se_forward(adv_tgt)
+        if tgt_emb is not None:
+            same = False
+            tgt_emb = self._tgt_emb(tgt_emb, B)
+        else:
+            same = vc_src.shape == vc_tgt.shape == adv_tgt.shape
+            tgt_emb = None if same else self.se_forward(adv_tgt)
         with self._lock:
             if same:
                 fn = {"e2e": lib().avc_e2e_attack, "fb": lib().avc_fb_attack}[kind]
@@ -368,6 +407,15 @@ class Context:
                           ctypes.c_void_p(tgt_emb.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()), B, T, float(eps),
                           int(n_iters), ctypes.c_void_p(out.data_ptr()), ctypes.byref(o), ctypes.c_void_p(stream)))
         return out, losses, grad0
+
+    def ws_stats(self) -> Dict[str, int]:
+        """avc_ws_stats: workspace builds / replans / hits, graph captures, evictions."""
+        v = [ctypes.c_int64() for _ in range(5)]
+        _check(lib().avc_ws_stats(self.h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("builds", "replans", "hits", "captures", "evictions"), (x.value for x in v)))
+
+    def set_ws_cache(self, n_shapes: int):
+        _check(lib().avc_set_ws_cache(self.h, int(n_shapes)))
 
     def set_engine(self, engine: str = "auto"):
         """"auto" | "layered" | "fused" | "long" (include/avc.h AVC_ENGINE_*)."""

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <list>
 #include <map>
 #include <string>
 #include <vector>
@@ -163,7 +164,7 @@ struct Workspace {
     hipGraphExec_t hdr_graph[2] = {nullptr, nullptr};
     DevBuf hdr, hdr_m, hdr_v, hdr_gx; // header [F*T], its Adam state, d loss / d x [N][F*T]
     bool built = false;
-    int gen = 0;                      // bumped whenever buffers / plans are rebuilt
+    int gen = 0;                      // ctx-unique id of this workspace's current plans (set on every (re)plan)
 };
 
 }  // namespace
@@ -202,7 +203,15 @@ struct avc_ctx {
     float* stage = nullptr;
     size_t stage_n = 0;
     hipEvent_t ev_stage = nullptr;
-    Workspace ws;
+    // Workspaces cached by shape: (B, T, engine) -> buffers + plans + captured graphs, most
+    // recently used first.  A call at a shape seen before re-plans nothing (real data: a stream of
+    // mixed-length utterances, and an adv_tgt embedded at its own length before the attack);
+    // the least recently used entry is freed past ws_cap entries.
+    std::list<Workspace> wss;
+    Workspace* cur = nullptr;           // the workspace of the call in progress
+    int ws_cap = 6;
+    int gen_next = 0;                   // source of Workspace::gen (unique over the ctx's life)
+    long n_ws_builds = 0, n_ws_replans = 0, n_ws_hits = 0, n_graph_captures = 0, n_ws_evictions = 0;
     bool profiling = false;
     std::map<std::string, std::pair<double, double>> prof;   // name -> (total ms, total flop)
     std::map<std::string, long> prof_n;
@@ -735,7 +744,9 @@ extern "C" void avc_destroy(avc_ctx* ctx) {
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     vc_free(ctx);
-    free_ws(ctx->ws);
+    for (Workspace& w : ctx->wss) free_ws(w);
+    ctx->wss.clear();
+    ctx->cur = nullptr;
     for (auto* v : {&ctx->AtF_bank, &ctx->AtF_c1, &ctx->AtF_c2, &ctx->AtB_c1, &ctx->AtB_c2, &ctx->bias_bank,
                     &ctx->bias_c1, &ctx->bias_c2})
         for (auto& b : *v) dfree(b);
@@ -853,8 +864,8 @@ static int add_gemm(avc_ctx* ctx, Plan& pl, std::vector<Problem> ps, double flop
         p.ksplit_rows = rup(cdiv(p.K, ksplit_req), KALIGN);
         ksplit = cdiv(p.K, p.ksplit_rows);
         if (ksplit > 1) {
-            if ((size_t)ksplit * p.M * p.N > ctx->ws.slab.n) return fail("internal: split-K slab too small");
-            p.slab = ctx->ws.slab.p;
+            if ((size_t)ksplit * p.M * p.N > ctx->cur->slab.n) return fail("internal: split-K slab too small");
+            p.slab = ctx->cur->slab.p;
         } else {
             p.ksplit_rows = 0;
         }
@@ -1283,12 +1294,16 @@ static int alloc_long(LongArgs& L, int B, int T, int nlayers) {
     L.fl_stride = (int64_t)((T + 32 + 15) / 16 + LZ_FL_EXTRA) * 4 * 2 * 64 * 4;
     L.nFmax = (T + 15) / 16;
     L.mask_stride = (int64_t)nlayers * L.nFmax * 32;
+    // each allocation is recorded in L at once, so free_ws releases a partial set on failure
     char* img = nullptr;
     float* fl = nullptr;
     unsigned long long* mk = nullptr;
     HIPCHK(hipMalloc(&img, 3 * (size_t)B * L.img_stride));
+    L.img[0] = img;
     HIPCHK(hipMalloc(&fl, 3 * (size_t)B * L.fl_stride * sizeof(float)));
+    L.fl[0] = fl;
     HIPCHK(hipMalloc(&mk, (size_t)B * L.mask_stride * sizeof(unsigned long long)));
+    L.masks = mk;
     // every byte a kernel may stage is finite from the start (weights past K are zero, and
     // 0 * NaN would not be)
     HIPCHK(hipMemset(img, 0, 3 * (size_t)B * L.img_stride));
@@ -1298,12 +1313,23 @@ static int alloc_long(LongArgs& L, int B, int T, int nlayers) {
         L.img[i] = img + (size_t)i * B * L.img_stride;
         L.fl[i] = fl + (size_t)i * B * L.fl_stride;
     }
-    L.masks = mk;
     return 0;
 }
 
+// a workspace whose build failed part-way: release what it holds and forget it (returns 1)
+static int drop_ws(avc_ctx* ctx) {
+    for (auto it = ctx->wss.begin(); it != ctx->wss.end(); ++it)
+        if (&*it == ctx->cur) {
+            (void)hipStreamSynchronize(ctx->stream);
+            free_ws(*it);
+            ctx->wss.erase(it);
+            break;
+        }
+    ctx->cur = nullptr;
+    return 1;
+}
+
 static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
-    Workspace& ws = ctx->ws;
     const avc_se_cfg& c = ctx->cfg;
     if (B <= 0) return fail("batch size must be positive (got %d)", B);
     // lengths through the blocks + reflect-pad validity (torch: pad < input length)
@@ -1328,19 +1354,42 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         Tl.push_back(To);
     }
     const int eng = engine_for(ctx, T);
-    const bool same = ws.built && ws.B == B && ws.T == T && ws.fused == (eng != AVC_ENGINE_LAYERED) &&
-                      ws.lz == (eng == AVC_ENGINE_LONG);
-    if (same && n_iters <= ws.iters_cap) return 0;
+    const bool fused = eng != AVC_ENGINE_LAYERED, lz = eng == AVC_ENGINE_LONG;
+    // a cached workspace of this shape (most recently used first)
+    auto it = ctx->wss.begin();
+    for (; it != ctx->wss.end(); ++it)
+        if (it->built && it->B == B && it->T == T && it->fused == fused && it->lz == lz) break;
+    if (it != ctx->wss.end()) {
+        ctx->wss.splice(ctx->wss.begin(), ctx->wss, it);
+        ctx->cur = &ctx->wss.front();
+        if (n_iters <= ctx->cur->iters_cap) {
+            ++ctx->n_ws_hits;
+            return 0;
+        }
+    } else {
+        // a new shape: make room (the stream may still use an evicted workspace's buffers)
+        const char* ce = getenv("AVC_WS_CACHE");
+        const int cap = std::max(1, ce ? atoi(ce) : ctx->ws_cap);
+        while ((int)ctx->wss.size() >= cap) {
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+            free_ws(ctx->wss.back());
+            ctx->wss.pop_back();
+            ++ctx->n_ws_evictions;
+        }
+        ctx->wss.emplace_front();
+        ctx->cur = &ctx->wss.front();
+    }
+    Workspace& ws = *ctx->cur;
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    if (!same) {
-        free_ws(ws);
+    if (!ws.built) {
+        ++ctx->n_ws_builds;
         ws.B = B;
         ws.T = T;
         ws.Tl = Tl;
         const int nb = ctx->nb;
         const size_t X = (size_t)B * c.c_in * T;
-        ws.fused = eng != AVC_ENGINE_LAYERED;
-        ws.lz = eng == AVC_ENGINE_LONG;
+        ws.fused = fused;
+        ws.lz = lz;
         int rc = 0;
         for (DevBuf* b : {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.grad0}) rc |= dalloc(*b, X);
         for (DevBuf* b : {&ws.emb_fwd, &ws.org, &ws.tgt}) rc |= dalloc(*b, (size_t)B * c.c_out);
@@ -1349,8 +1398,9 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
             rc |= dalloc(ws.pooled, (size_t)B * FZ_C);
             rc |= dalloc(ws.gpooled, (size_t)B * FZ_C);
             rc |= dalloc(ws.loss_cur, (size_t)B);
+            if (rc) return drop_ws(ctx);
             HIPCHK(hipMalloc(&ws.masks, (size_t)B * ws.mask_words * sizeof(unsigned long long)));
-            if (ws.lz && alloc_long(ws.lza, B, T, nb + 1 + 2 * c.n_conv_blocks)) return 1;
+            if (ws.lz && alloc_long(ws.lza, B, T, nb + 1 + 2 * c.n_conv_blocks)) return drop_ws(ctx);
         } else {
             rc |= dalloc(ws.gxd, X);
             rc |= dalloc(ws.bank, (size_t)B * nb * c.c_bank * T);
@@ -1367,28 +1417,31 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
             }
             rc |= dalloc(ws.slab, (size_t)KSPLIT_MAX * std::max(c.c_h, c.c_in) * B * T);
         }
+        if (rc) return drop_ws(ctx);
         HIPCHK(hipMalloc(&ws.step, sizeof(int)));
-        rc |= dalloc(ws.scal, 8);
-        if (rc) return 1;
+        if (dalloc(ws.scal, 8)) return drop_ws(ctx);
+    } else {
+        ++ctx->n_ws_replans;   // more iterations than this workspace's tables hold
     }
     const int cap = std::max(n_iters, std::max(ws.iters_cap, 1));
-    if (dalloc(ws.losses, (size_t)cap * B)) return 1;
-    if (dalloc(ws.table, (size_t)cap * 2)) return 1;
+    if (dalloc(ws.losses, (size_t)cap * B)) return drop_ws(ctx);
+    if (dalloc(ws.table, (size_t)cap * 2)) return drop_ws(ctx);
     ws.iters_cap = cap;
     // (re)build plans: pointers may have moved (the bf16 plan is rebuilt on demand)
     free_plans(ws);
-    ++ws.gen;
+    ws.built = false;
+    ws.gen = ++ctx->gen_next;
     if (ws.fused) {
-        if (plan_fused_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return 1;
+        if (plan_fused_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return drop_ws(ctx);
     } else {
-        if (plan_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return 1;
+        if (plan_forward(ctx, ws, ws.fwd, ws.xin.p, false, PREC_F32)) return drop_ws(ctx);
     }
-    if (plan_iteration(ctx, ws, ws.iter, PREC_F32)) return 1;
+    if (plan_iteration(ctx, ws, ws.iter, PREC_F32)) return drop_ws(ctx);
     // autotune with a valid Adam step (1) and eps/gscale (the kernels clamp anyway)
     const float scal0[8] = {0.1f, 0.f, 0.f, 0.f, 0.1f, 0.f, 0.f, 0.f};
     HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
     HIPCHK(hipMemset(ws.step, 0, sizeof(int)));
-    if (autotune(ctx, ws.fwd) || autotune(ctx, ws.iter)) return 1;
+    if (autotune(ctx, ws.fwd) || autotune(ctx, ws.iter)) return drop_ws(ctx);
     ws.built = true;
     return 0;
 }
@@ -1533,8 +1586,8 @@ static std::string kernel_name(const Launch& L) {
 static std::string tune_key(avc_ctx* ctx, const Plan& pl, size_t li) {
     char buf[256];
     const avc_se_cfg& c = ctx->cfg;
-    snprintf(buf, sizeof(buf), "B%d_T%d_ch%d_%d_%d_nb%d_%s_l%zu", ctx->ws.B, ctx->ws.T, c.c_in, c.c_h, c.c_bank,
-             c.n_conv_blocks, &pl == &ctx->ws.fwd ? "fwd" : (&pl == &ctx->ws.iter ? "iter" : "iterbf16"), li);
+    snprintf(buf, sizeof(buf), "B%d_T%d_ch%d_%d_%d_nb%d_%s_l%zu", ctx->cur->B, ctx->cur->T, c.c_in, c.c_h, c.c_bank,
+             c.n_conv_blocks, &pl == &ctx->cur->fwd ? "fwd" : (&pl == &ctx->cur->iter ? "iter" : "iterbf16"), li);
     return buf;
 }
 
@@ -1555,7 +1608,7 @@ static std::map<std::string, int> read_tune_file() {
 // kernel, grid, split-K) -- lets a rocprofv3 trace be read layer by layer.
 static void print_plan(avc_ctx* ctx, const Plan& pl) {
     if (!getenv("AVC_PRINT_PLAN")) return;
-    const char* tag = &pl == &ctx->ws.fwd ? "fwd" : (&pl == &ctx->ws.iter ? "iter" : "iterbf16");
+    const char* tag = &pl == &ctx->cur->fwd ? "fwd" : (&pl == &ctx->cur->iter ? "iter" : "iterbf16");
     for (size_t i = 0; i < pl.launches.size(); ++i) {
         const Launch& L = pl.launches[i];
         const dim3 g = L.kind == L_GEMM ? gemm_grid(L, L.variant) : L.grid;
@@ -1677,7 +1730,7 @@ extern "C" int avc_se_forward(avc_ctx* ctx, const float* x, int B, int T, float*
     hipStream_t us = (hipStream_t)stream;
     if (ensure_ws(ctx, B, T, 1)) return 1;
     if (begin_call(ctx, us)) return 1;
-    Workspace& ws = ctx->ws;
+    Workspace& ws = *ctx->cur;
     const avc_se_cfg& c = ctx->cfg;
     HIPCHK(hipMemcpyAsync(ws.xin.p, x, (size_t)B * c.c_in * T * sizeof(float), hipMemcpyDeviceToDevice,
                           ctx->stream));
@@ -1717,8 +1770,8 @@ extern "C" int avc_set_profiling(avc_ctx* ctx, int enable) {
 // scalars [eps, loss-grad scales...] -> ws.table / ws.scal on ctx->stream, asynchronously
 // through the pinned staging buffer
 static int stage_call_consts(avc_ctx* ctx, int n_iters, const float scal[4], double lr = 1e-3, double beta1 = 0.9,
-                             double beta2 = 0.999, float lam = 0.1f) {
-    Workspace& ws = ctx->ws;
+                             double beta2 = 0.999, float lam = 0.1f, int t0 = 0) {
+    Workspace& ws = *ctx->cur;
     const size_t nt = 2 * (size_t)std::max(n_iters, 1);
     HIPCHK(hipEventSynchronize(ctx->ev_stage));   // the previous call's staging copies are done
     if (ctx->stage_n < nt + 8) {
@@ -1730,9 +1783,9 @@ static int stage_call_consts(avc_ctx* ctx, int n_iters, const float scal[4], dou
     }
     float* table = ctx->stage;
     for (size_t i = 0; i < nt; ++i) table[i] = 0.f;
-    for (int t = 1; t <= n_iters; ++t) {
-        const double bc1 = 1.0 - std::pow(beta1, t);
-        const double bc2 = 1.0 - std::pow(beta2, t);
+    for (int t = 1; t <= n_iters; ++t) {   // step t0 + t of the optimiser (t0 steps taken before this call)
+        const double bc1 = 1.0 - std::pow(beta1, t0 + t);
+        const double bc2 = 1.0 - std::pow(beta2, t0 + t);
         table[2 * (t - 1)] = (float)(-(lr / bc1));
         table[2 * (t - 1) + 1] = (float)std::sqrt(bc2);
     }
@@ -1759,8 +1812,10 @@ static int graph_replay(avc_ctx* ctx, Plan& iter, hipGraphExec_t& graph, int n_i
         int rc = 0;
         for (int it = 0; it < GRAPH_ITERS && !rc; ++it) rc = run_plan(ctx, iter, false);
         hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        if (e == hipSuccess && rc) (void)hipGraphDestroy(g);
         if (rc) return 1;
         if (e != hipSuccess) return fail("graph capture: %s", hipGetErrorString(e));
+        ++ctx->n_graph_captures;
         e = hipGraphInstantiate(&graph, g, nullptr, nullptr, 0);
         (void)hipGraphDestroy(g);
         if (e != hipSuccess) {
@@ -1791,7 +1846,7 @@ static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_t
         return fail("bad update %d (PGD needs pgd_step > 0)", o.update);
     hipStream_t us = (hipStream_t)stream;
     if (ensure_ws(ctx, B, T, n_iters)) return 1;
-    Workspace& ws = ctx->ws;
+    Workspace& ws = *ctx->cur;
     const bool bf16 = o.precision == AVC_PREC_BF16;
     if (bf16 && ws.iter_bf16.launches.empty()) {
         // the setup below rewrites eps and the step counter with blocking copies on the null
@@ -1916,18 +1971,22 @@ static int plan_header(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec, int N, i
     return 0;
 }
 
-extern "C" int avc_header_optimize(avc_ctx* ctx, const float* source, const float* target, int N, int T,
-                                   float* header, float epsilon, float lambda_param, float lr, float beta1,
-                                   float beta2, float adam_eps, int n_iters, int precision, float* losses,
-                                   void* stream) {
+static int header_optimize_impl(avc_ctx* ctx, const float* source, const float* target, int N, int T, float* header,
+                                float epsilon, float lambda_param, float lr, float beta1, float beta2, float adam_eps,
+                                int n_iters, int precision, float* losses, float* exp_avg, float* exp_avg_sq,
+                                int step0, void* stream) {
     if (!ctx || !source || !target || !header) return fail("avc_header_optimize: null argument");
     if (n_iters < 0) return fail("n_iters must be >= 0");
+    if (step0 < 0) return fail("avc_header_optimize_state: step0 must be >= 0");
+    if ((exp_avg == nullptr) != (exp_avg_sq == nullptr))
+        return fail("avc_header_optimize_state: give both exp_avg and exp_avg_sq, or neither");
+    if (step0 > 0 && !exp_avg) return fail("avc_header_optimize_state: step0 > 0 needs the Adam moments");
     if (precision != AVC_PREC_FP32 && precision != AVC_PREC_BF16) return fail("bad precision %d", precision);
     if (!(lr > 0.f) || !(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) || !(adam_eps >= 0.f))
         return fail("avc_header_optimize: bad Adam hyper-parameters");
     hipStream_t us = (hipStream_t)stream;
     if (ensure_ws(ctx, N, T, n_iters)) return 1;
-    Workspace& ws = ctx->ws;
+    Workspace& ws = *ctx->cur;
     if (!ws.fused) return fail("the header optimiser runs on the fused / long engine (not LAYERED)");
     const avc_se_cfg& c = ctx->cfg;
     const int FT = c.c_in * T;
@@ -1956,7 +2015,7 @@ extern "C" int avc_header_optimize(avc_ctx* ctx, const float* source, const floa
     if (begin_call(ctx, us)) return 1;
     const float gscale = (float)(2.0 / ((double)N * c.c_out));
     const float scal[4] = {epsilon, gscale, 0.f, 0.f};
-    if (stage_call_consts(ctx, n_iters, scal, lr, beta1, beta2, lambda_param)) return 1;
+    if (stage_call_consts(ctx, n_iters, scal, lr, beta1, beta2, lambda_param, step0)) return 1;
     // source_embedding = SE(source), target_embedding = SE(target)   (header_model.py:48-49)
     HIPCHK(hipMemcpyAsync(ws.vc.p, source, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(ws.xin.p, source, X * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
@@ -1968,15 +2027,40 @@ extern "C" int avc_header_optimize(avc_ctx* ctx, const float* source, const floa
     HIPCHK(hipMemcpyAsync(ws.tgt.p, ws.emb_fwd.p, (size_t)N * c.c_out * sizeof(float), hipMemcpyDeviceToDevice,
                           ctx->stream));
     HIPCHK(hipMemcpyAsync(ws.hdr.p, header, FT * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
-    HIPCHK(hipMemsetAsync(ws.hdr_m.p, 0, FT * sizeof(float), ctx->stream));
-    HIPCHK(hipMemsetAsync(ws.hdr_v.p, 0, FT * sizeof(float), ctx->stream));
+    if (exp_avg) {   // the caller's optimiser state (torch Adam exp_avg / exp_avg_sq)
+        HIPCHK(hipMemcpyAsync(ws.hdr_m.p, exp_avg, FT * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(ws.hdr_v.p, exp_avg_sq, FT * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+        HIPCHK(hipMemsetAsync(ws.hdr_m.p, 0, FT * sizeof(float), ctx->stream));
+        HIPCHK(hipMemsetAsync(ws.hdr_v.p, 0, FT * sizeof(float), ctx->stream));
+    }
     HIPCHK(hipMemsetAsync(ws.step, 0, sizeof(int), ctx->stream));
     if (run_iterations(ctx, pl, graph, n_iters, true)) return 1;
     HIPCHK(hipMemcpyAsync(header, ws.hdr.p, FT * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    if (exp_avg) {
+        HIPCHK(hipMemcpyAsync(exp_avg, ws.hdr_m.p, FT * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(exp_avg_sq, ws.hdr_v.p, FT * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    }
     if (losses && n_iters > 0)
         HIPCHK(hipMemcpyAsync(losses, ws.losses.p, (size_t)n_iters * N * sizeof(float), hipMemcpyDeviceToDevice,
                               ctx->stream));
     return end_call(ctx, us);
+}
+
+extern "C" int avc_header_optimize(avc_ctx* ctx, const float* source, const float* target, int N, int T,
+                                   float* header, float epsilon, float lambda_param, float lr, float beta1,
+                                   float beta2, float adam_eps, int n_iters, int precision, float* losses,
+                                   void* stream) {
+    return header_optimize_impl(ctx, source, target, N, T, header, epsilon, lambda_param, lr, beta1, beta2, adam_eps,
+                                n_iters, precision, losses, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int avc_header_optimize_state(avc_ctx* ctx, const float* source, const float* target, int N, int T,
+                                         float* header, float epsilon, float lambda_param, float lr, float beta1,
+                                         float beta2, float adam_eps, int n_iters, int precision, float* losses,
+                                         float* exp_avg, float* exp_avg_sq, int step0, void* stream) {
+    return header_optimize_impl(ctx, source, target, N, T, header, epsilon, lambda_param, lr, beta1, beta2, adam_eps,
+                                n_iters, precision, losses, exp_avg, exp_avg_sq, step0, stream);
 }
 
 extern "C" int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_flop_per_iter) {
@@ -1987,6 +2071,24 @@ extern "C" int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_f
     for (auto& kv : ctx->prof)
         if (kv.first.rfind("role:", 0) != 0) f += kv.second.second;
     if (gemm_flop_per_iter) *gemm_flop_per_iter = f / ctx->prof_iters;
+    return 0;
+}
+
+extern "C" int avc_ws_stats(avc_ctx* ctx, int64_t* builds, int64_t* replans, int64_t* hits, int64_t* captures,
+                            int64_t* evictions) {
+    if (!ctx) return fail("null ctx");
+    if (builds) *builds = ctx->n_ws_builds;
+    if (replans) *replans = ctx->n_ws_replans;
+    if (hits) *hits = ctx->n_ws_hits;
+    if (captures) *captures = ctx->n_graph_captures;
+    if (evictions) *evictions = ctx->n_ws_evictions;
+    return 0;
+}
+
+extern "C" int avc_set_ws_cache(avc_ctx* ctx, int n_shapes) {
+    if (!ctx) return fail("null ctx");
+    if (n_shapes < 1 || n_shapes > 64) return fail("avc_set_ws_cache: n_shapes must be in [1, 64] (got %d)", n_shapes);
+    ctx->ws_cap = n_shapes;
     return 0;
 }
 

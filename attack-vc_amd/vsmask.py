@@ -51,8 +51,10 @@ class UniversalPerturbationHeader:
 
         source_mel / target_mel: [N, 1, F, T] as train_header.py builds them (or [N, F, T]; the
         reference's SpeakerEncoder cannot take the 4-D form, SURVEY.md 2 note A).  The header
-        is updated in place; `optimizer`'s own state is not advanced (its hyper-parameters are
-        read from param_groups[0]).  Prints the batch loss every 100 iterations like the
+        is updated in place, and `optimizer` advances exactly as torch's Adam would: its
+        hyper-parameters come from param_groups[0], its state for the header (exp_avg,
+        exp_avg_sq, step) is continued and written back, so repeated calls with one optimizer
+        follow the reference's trajectory.  Prints the batch loss every 100 iterations like the
         reference."""
         def mel3(x):
             return x[:, 0] if x.dim() == 4 else x
@@ -62,10 +64,26 @@ class UniversalPerturbationHeader:
             raise RuntimeError("libavc implements plain Adam (no amsgrad / weight_decay / maximize)")
         ctx = avc_native.context_for(speaker_encoder, src.device)
         hdr0 = self.header.detach()[0, 0]
+        # torch Adam's per-parameter state for the header (created on its first step)
+        st = optimizer.state[self.header] if self.header in optimizer.state else {}
+        if st:
+            m = st["exp_avg"].detach()[0, 0].float().contiguous().clone()
+            v = st["exp_avg_sq"].detach()[0, 0].float().contiguous().clone()
+            step0 = int(st["step"])
+        else:
+            m = torch.zeros_like(hdr0, dtype=torch.float32)
+            v = torch.zeros_like(hdr0, dtype=torch.float32)
+            step0 = 0
         new, losses = ctx.header_optimize(src, tgt, hdr0, int(num_iterations), epsilon, lambda_param, g["lr"],
-                                          g["betas"], g["eps"], precision)
+                                          g["betas"], g["eps"], precision, adam_state=(m, v, step0))
         with torch.no_grad():
             self.header.data.copy_(new.reshape(self.header.shape))
+        if int(num_iterations) > 0:
+            shape = self.header.shape
+            optimizer.state[self.header] = {
+                "step": torch.tensor(float(step0 + int(num_iterations))),
+                "exp_avg": m.reshape(shape).to(self.header.dtype),
+                "exp_avg_sq": v.reshape(shape).to(self.header.dtype)}
         batch = losses.mean(dim=1).cpu()
         for i in range(99, int(num_iterations), 100):
             print(f"Iteration {i+1}/{num_iterations}, Loss: {batch[i].item():.6f}")

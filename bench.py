@@ -106,7 +106,27 @@ def launch_ranks(a) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    codes = [p.wait() for p in procs]
+    # poll: the first rank to fail ends the others (they would otherwise wait in the rendezvous or
+    # a barrier until gloo's 30-minute timeout)
+    codes = [None] * len(procs)
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            break
+        time.sleep(0.2)
     return max(codes, key=abs)
 
 
@@ -256,7 +276,7 @@ def main_pm(a):
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")   # host-side barrier / max only: no RCCL in the process
     import predictive_model
     import shard
     torch.manual_seed(0)
@@ -279,7 +299,7 @@ def main_pm(a):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, None)
     assert torch.isfinite(y).all()
     cpu = cpu_baseline_pm(min(a.cpu_seconds, 10.0), sd) if rank == 0 and world == 1 and not a.no_cpu_baseline else None
     if rank == 0:
@@ -328,7 +348,7 @@ def main_mel2wav(a):
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")   # host-side barrier / max only: no RCCL in the process
     import data_utils
     import shard
     B, T = a.batch, a.frames
@@ -356,7 +376,7 @@ def main_mel2wav(a):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, None)
     assert torch.isfinite(out).all()
     roof = None
     if not a.no_roofline:
@@ -442,7 +462,7 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")   # host-side barrier / max only: no RCCL in the process
 
     import attack_utils
     import avc_native
@@ -482,7 +502,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, None)
     assert torch.isfinite(out).all()
 
     fp32_cmp = None
@@ -497,7 +517,7 @@ def main():
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
-        e32 = shard.max_over_ranks(time.perf_counter() - t1, dist, dev)
+        e32 = shard.max_over_ranks(time.perf_counter() - t1, dist, None)
         fp32_cmp = {"value": round(total / e32, 3), "ms_per_step": round(e32 * 1e3, 3),
                     "max_abs_diff_vs_bf16": float((out32 - out).detach().abs().max())}
 

@@ -228,6 +228,15 @@ int avc_header_optimize(avc_ctx* ctx, const float* source, const float* target, 
                         float epsilon, float lambda_param, float lr, float beta1, float beta2, float adam_eps,
                         int n_iters, int precision, float* losses, void* stream);
 
+/* The same, continuing a torch Adam optimiser: exp_avg / exp_avg_sq [80][T] device (in: its
+ * state before the call, out: after; both or neither), step0 = the steps it has taken (its
+ * state["step"]; the bias corrections continue from step0 + 1).  The reference passes one
+ * optimizer whose state carries across optimize() calls (header_model.py:25-68). */
+int avc_header_optimize_state(avc_ctx* ctx, const float* source, const float* target, int N, int T, float* header,
+                              float epsilon, float lambda_param, float lr, float beta1, float beta2, float adam_eps,
+                              int n_iters, int precision, float* losses, float* exp_avg, float* exp_avg_sq,
+                              int step0, void* stream);
+
 /* UniversalPerturbationHeader.apply_header (header_model.py:70-95):
  * out = clamp(mel + header on frames [0, min(T, Th)), -1, 1). */
 int avc_vsmask_apply_header(int device, const float* mel, int B, int F, int T, const float* header, int Th,
@@ -297,6 +306,20 @@ int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_flop_per_ite
 int avc_profile_kernel_count(avc_ctx* ctx);
 int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len, long* launches, double* total_ms,
                        double* total_flop);
+
+/* Workspace cache of a context.  A context keeps the buffers, launch plans and captured hipGraphs
+ * of the last few (B, T, engine) shapes it ran (6 by default; env AVC_WS_CACHE overrides), most
+ * recently used first, so a call at a shape seen before neither synchronises, allocates, plans nor
+ * captures (real data: length-bucketed batches, an adv_tgt embedded at its own length).  Counters
+ * since avc_create (any pointer may be NULL):
+ *   builds   workspaces allocated and planned for a new shape
+ *   replans  a cached workspace re-planned because a call needed more iterations than it holds
+ *   hits     calls served by a cached workspace as it was
+ *   captures hipGraphs captured (attack loops, header optimiser)
+ *   evictions cached workspaces freed to make room */
+int avc_ws_stats(avc_ctx* ctx, int64_t* builds, int64_t* replans, int64_t* hits, int64_t* captures,
+                 int64_t* evictions);
+int avc_set_ws_cache(avc_ctx* ctx, int n_shapes);
 
 const char* avc_last_error(void);
 const char* avc_version(void);

@@ -67,3 +67,27 @@ def test_header_optimize_module_bf16_and_shapes(full):
     with pytest.raises(RuntimeError):
         avc_native.context_for(m.speaker_encoder, DEV).header_optimize(
             torch.from_numpy(src).to(DEV), torch.from_numpy(tgt).to(DEV), torch.zeros(80, T - 1, device=DEV), 1)
+
+
+def test_header_optimize_continues_optimizer_state(full):
+    """One torch Adam optimiser across optimize() calls, as the reference's (header_model.py:25-68):
+    4 + 4 iterations equal 8 iterations bit for bit (moments and bias-correction step carried
+    through optimizer.state), and the optimiser's state records the 8 steps."""
+    m, _, _ = full
+    m = m.to(DEV)
+    N, T = 2, 100
+    src, tgt = _mels(N, T, 4)
+    s4, t4 = torch.from_numpy(src).to(DEV)[:, None], torch.from_numpy(tgt).to(DEV)[:, None]
+    a = vsmask.UniversalPerturbationHeader(device="cuda:0")
+    b = vsmask.UniversalPerturbationHeader(device="cuda:0")
+    with torch.no_grad():
+        b.header.copy_(a.header)
+    oa = torch.optim.Adam([a.header], lr=2e-3)
+    ob = torch.optim.Adam([b.header], lr=2e-3)
+    a.optimize(s4, t4, m.speaker_encoder, oa, num_iterations=8, epsilon=0.08)
+    b.optimize(s4, t4, m.speaker_encoder, ob, num_iterations=4, epsilon=0.08)
+    b.optimize(s4, t4, m.speaker_encoder, ob, num_iterations=4, epsilon=0.08)
+    assert torch.equal(a.header.detach(), b.header.detach())
+    assert int(ob.state[b.header]["step"]) == 8
+    assert torch.equal(oa.state[a.header]["exp_avg"], ob.state[b.header]["exp_avg"])
+    assert torch.equal(oa.state[a.header]["exp_avg_sq"], ob.state[b.header]["exp_avg_sq"])
