@@ -1,5 +1,5 @@
 #!/bin/bash
-# One gpurun call of round 2: GPU tests (selectable), smoke, and the default bench line.
+# One gpurun call: GPU tests (selectable), smoke, and the default bench line.
 # Every GPU step runs under its own time limit; the first failure / crash / timeout ends it.
 #   TESTS="tests/test_gpu_lengths.py ..." (default: all -m gpu)   SMOKE=1   BENCH=1   EXTRA="cmd"
 set -u
