@@ -32,6 +32,22 @@ TOL_ADV = {1: 1e-5, 10: 1e-4, 100: 1e-3, 1500: 5e-3}
 TOL_ADV_MEAN = {1: 1e-8, 10: 1e-7, 100: 1e-6, 1500: 1e-4}
 
 
+def check_grad_flip_robust(g, ref, frac=0.05):
+    """d loss / d ptb vs a float64 restatement where an isolated ReLU / LeakyReLU mask may flip:
+    a pre-activation within fp32 rounding of zero (measured: 4.9e-9 of its layer's max at T=176,
+    seed 876, conv_bank k=7, frame 164) takes the other branch in fp32, which changes the
+    gradient over that unit's receptive field only (8-80 columns of one utterance, up to 7e-3 of
+    max |grad| there).  So: every utterance normwise within TOL_VC_GRAD_L2_MAX, and all but `frac`
+    of the elements within TOL_GRAD_REL of max |grad| (a systematic error breaks both)."""
+    g = np.asarray(g, np.float64)
+    ref = np.asarray(ref, np.float64)
+    for u in range(g.shape[0]):
+        e = float(np.linalg.norm(g[u] - ref[u]) / np.linalg.norm(ref[u]))
+        assert e <= TOL_VC_GRAD_L2_MAX, (u, e)
+    off = np.abs(g - ref) > TOL_GRAD_REL * np.abs(ref).max()
+    assert off.mean() <= frac, off.mean()
+
+
 def check_adv(adv, ref, n):
     d = np.abs(np.asarray(adv, np.float64) - np.asarray(ref, np.float64))
     assert d.max() <= TOL_ADV[n], (n, d.max())

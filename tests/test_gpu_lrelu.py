@@ -52,7 +52,7 @@ def test_lrelu_long_engine_vs_oracle(lrelu, T):
     from the ballot words) vs the float64 oracle: SpeakerEncoder(x), the emb attack's grad0 /
     10-iteration adv / losses, inference, and the e2e / fb iteration-0 gradients (normwise per
     utterance, helpers.TOL_VC_GRAD_*).  vc_src / adv_tgt of other lengths on the way."""
-    from helpers import TOL_VC_GRAD_L2_MAX, TOL_VC_GRAD_L2_MEDIAN, cfg_of
+    from helpers import TOL_VC_GRAD_L2_MAX, TOL_VC_GRAD_L2_MEDIAN, cfg_of, check_grad_flip_robust
     from oracle import adain_vc as oracle
     z, m = lrelu
     ctx = avc_native.context_for(m.speaker_encoder, DEV)
@@ -73,7 +73,9 @@ def test_lrelu_long_engine_vs_oracle(lrelu, T):
     adv, info = attack_utils.emb_attack(m, d(vc), d(at), 0.1, 10, ptb0=d(p0), return_info=True)
     rec = {}
     ref = oracle.emb_attack(w64, cfg, f64(vc), f64(at), 0.1, 10, f64(p0), record=rec)
-    assert rel(info["grad0"].cpu().numpy(), rec["grad0"]) <= TOL_GRAD_REL
+    # mask flips at near-zero pre-activations (helpers.check_grad_flip_robust): seed 900's
+    # utterance 1 at T = 200 has one, 2.8e-3 of max |grad| over columns 1-12
+    check_grad_flip_robust(info["grad0"].cpu().numpy(), rec["grad0"])
     check_adv(adv.detach().cpu().numpy(), ref, 10)
     np.testing.assert_allclose(info["losses"].cpu().numpy().T, rec["losses"], rtol=2e-4, atol=1e-9)
     out = m.inference(d(src), d(vc)).cpu().numpy()
