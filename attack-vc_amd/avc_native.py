@@ -88,6 +88,11 @@ SIGNATURES = [
     ("avc_vc_weight_count", ctypes.c_size_t, [ctypes.POINTER(VCCfg)]),
     ("avc_attach_vc", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(VCCfg), ctypes.c_void_p, ctypes.c_size_t]),
     ("avc_vc_out_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("avc_content_encoder", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_content_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("avc_decoder", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_inference", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_inference_emb", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -342,6 +347,42 @@ class Context:
         if n < 0:
             raise RuntimeError(lib().avc_last_error().decode(errors="replace"))
         return n
+
+    def content_encoder(self, x: torch.Tensor):
+        """ContentEncoder.forward (models.py:181-210): x [B, 80, T] -> (mu, log_sigma) [B, c_out, Tce]."""
+        _require_gpu(x)
+        x = x.contiguous()
+        self._check_mel("x", x, self.cfg["c_in"])
+        B, _, T = x.shape
+        n = lib().avc_content_frames(self.h, int(T))
+        if n < 0:
+            _check(1)
+        mu = torch.empty(B, self._vcs.ce_c_out, n, device=x.device)
+        ls = torch.empty_like(mu)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_content_encoder(self.h, ctypes.c_void_p(x.data_ptr()), B, T, ctypes.c_void_p(mu.data_ptr()),
+                                             ctypes.c_void_p(ls.data_ptr()), ctypes.c_void_p(stream)))
+        return mu, ls
+
+    def decoder(self, z: torch.Tensor, cond: torch.Tensor) -> torch.Tensor:
+        """Decoder.forward (models.py:403-435): z [B, 128, Tz], cond [B, 128] -> [B, 80, Tz * prod(upsample)]."""
+        _require_gpu(z, cond)
+        z, cond = z.contiguous(), cond.contiguous()
+        if z.dim() != 3 or z.shape[1] != self._vcs.dec_c_in:
+            raise RuntimeError(f"z: expected [B, {self._vcs.dec_c_in}, T], got {tuple(z.shape)}")
+        B, _, Tz = z.shape
+        if tuple(cond.shape) != (B, self._vcs.dec_c_cond):
+            raise RuntimeError(f"cond: expected [{B}, {self._vcs.dec_c_cond}], got {tuple(cond.shape)}")
+        up = 1
+        for i in range(self._vcs.dec_n_conv_blocks):
+            up *= int(self._vcs.dec_upsample[i])
+        out = torch.empty(B, self._vcs.dec_c_out, Tz * up, device=z.device)
+        stream = torch.cuda.current_stream(z.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_decoder(self.h, ctypes.c_void_p(z.data_ptr()), B, Tz, ctypes.c_void_p(cond.data_ptr()),
+                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+        return out
 
     def inference(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
         """AdaInVC.inference: the output takes src's length (models.py:472-489); a tgt of another

@@ -10,13 +10,35 @@ Drop-in for /root/reference/models.py:121-485 as far as the attack path needs:
 
   * ``inference(src, tgt)`` (models.py:472-489) runs ContentEncoder ->
     SpeakerEncoder -> Decoder as libavc's fused HIP kernels (avc_vc.hip);
-    ContentEncoder / Decoder otherwise only hold their parameters (the e2e / fb
-    attacks hand them to libavc once, avc_attach_vc).
+  * ``content_encoder(x)`` -> (mu, log_sigma) (models.py:181-210) and
+    ``decoder(z, cond)`` (models.py:403-435) run the same kernels on their own.
+    Their weights are handed to libavc together with the speaker encoder's (the
+    libavc context of the AdaInVC they belong to, avc_attach_vc), so these two
+    forwards need the module to sit in an AdaInVC, as the reference uses them.
 """
+import weakref
 from typing import Dict, List
 
 import torch
 import torch.nn as nn
+
+
+class _InModel:
+    """Back-reference to the AdaInVC a ContentEncoder / Decoder belongs to (weak: no cycle, not in
+    the state_dict, dropped when pickled)."""
+
+    def _avc_model(self):
+        ref = self.__dict__.get("_avc_parent")
+        m = ref() if ref is not None else None
+        if m is None:
+            raise RuntimeError(f"{type(self).__name__}.forward runs on libavc through the AdaInVC it belongs to "
+                               "(its weights are attached with the speaker encoder's); build it inside AdaInVC")
+        return m
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st.pop("_avc_parent", None)
+        return st
 
 
 def _act_code(act: str) -> int:
@@ -24,8 +46,8 @@ def _act_code(act: str) -> int:
     return 1 if act == "lrelu" else 0
 
 
-class ContentEncoder(nn.Module):
-    """Parameter tree of models.py:121-179 (same registration order)."""
+class ContentEncoder(_InModel, nn.Module):
+    """Parameter tree of models.py:121-179 (same registration order); forward -> (mu, log_sigma)."""
 
     def __init__(self, c_in: int, c_h: int, c_out: int, kernel_size: int, bank_size: int,
                  bank_scale: int, c_bank: int, n_conv_blocks: int, subsample: List[int],
@@ -53,6 +75,11 @@ class ContentEncoder(nn.Module):
 
     def avc_config(self) -> Dict:
         return dict(self._cfg)
+
+    def forward(self, x: torch.Tensor):
+        """models.py:181-210 on libavc (fp32): x [B, 80, T] -> (mu, log_sigma) [B, c_out, ceil-pooled T]."""
+        from avc_native import vc_context_for
+        return vc_context_for(self._avc_model(), x.device).content_encoder(x)
 
 
 class SpeakerEncoder(nn.Module):
@@ -96,8 +123,8 @@ class SpeakerEncoder(nn.Module):
         return speaker_encoder_forward(self, x)
 
 
-class Decoder(nn.Module):
-    """Parameter tree of models.py:346-401 (sn=False only)."""
+class Decoder(_InModel, nn.Module):
+    """Parameter tree of models.py:346-401 (sn=False only); forward(z, cond)."""
 
     def __init__(self, c_in: int, c_cond: int, c_h: int, c_out: int, kernel_size: int,
                  n_conv_blocks: int, upsample: List[int], act: str, sn: bool, dropout_rate: float):
@@ -123,6 +150,11 @@ class Decoder(nn.Module):
     def avc_config(self) -> Dict:
         return dict(self._cfg)
 
+    def forward(self, z: torch.Tensor, cond: torch.Tensor) -> torch.Tensor:
+        """models.py:403-435 on libavc (fp32): z [B, c_in, T], cond [B, c_cond] -> [B, c_out, T * prod(upsample)]."""
+        from avc_native import vc_context_for
+        return vc_context_for(self._avc_model(), z.device).decoder(z, cond)
+
 
 class AdaInVC(nn.Module):
     """models.py:438-452 module tree: content_encoder, speaker_encoder, decoder."""
@@ -133,6 +165,15 @@ class AdaInVC(nn.Module):
         self.content_encoder = ContentEncoder(**config["ContentEncoder"])
         self.speaker_encoder = SpeakerEncoder(**config["SpeakerEncoder"])
         self.decoder = Decoder(**config["Decoder"])
+        self._avc_link()
+
+    def _avc_link(self):
+        for m in (self.content_encoder, self.decoder):
+            object.__setattr__(m, "_avc_parent", weakref.ref(self))
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        self._avc_link()
 
     def inference(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
         """AdaInVC.inference (models.py:472-489): Decoder(ContentEncoder(src).mu,

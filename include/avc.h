@@ -162,6 +162,15 @@ int avc_inference(avc_ctx* ctx, const float* src, const float* tgt, int B, int T
 int avc_inference_emb(avc_ctx* ctx, const float* src, int B, int T_src, const float* emb, float* out,
                       void* stream);
 
+/* ContentEncoder.forward (models.py:181-210): mu, log_sigma [B, c_out, Tce] (either may be NULL) of
+ * x [B, c_in, T]; Tce = avc_content_frames(T).  fp32. */
+int avc_content_encoder(avc_ctx* ctx, const float* x, int B, int T, float* mu, float* log_sigma, void* stream);
+int avc_content_frames(avc_ctx* ctx, int T);
+
+/* Decoder.forward (models.py:403-435): out [B, c_out, Tz * prod(upsample)] = Decoder(z [B, c_in, Tz],
+ * cond [B, c_cond]).  fp32. */
+int avc_decoder(avc_ctx* ctx, const float* z, int B, int Tz, const float* cond, float* out, void* stream);
+
 /* End-to-end attack (attack_utils.py:7-48) and feedback attack (attack_utils.py:89-130):
  * same buffers and options as avc_emb_attack plus vc_src [B, c_in, T].  losses (optional)
  * [n_iters, B]: e2e MSE(dec, tgt_out) - 0.1 MSE(dec, org_out); fb MSE(SE(dec), tgt_emb) -

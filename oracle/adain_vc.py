@@ -224,8 +224,9 @@ def se_backward(w, cfg, st, g_emb, p="speaker_encoder."):
 # ----------------------------------------------------------------------------------
 
 
-def ce_forward(w, cfg, x, p="content_encoder."):
-    """ContentEncoder.forward -> mu (models.py:181-208; log_sigma unused by inference)."""
+def ce_forward(w, cfg, x, p="content_encoder.", log_sigma=False):
+    """ContentEncoder.forward -> mu (models.py:181-208; log_sigma unused by inference), or
+    (mu, log_sigma) (models.py:208-210) with log_sigma=True."""
     relu, _ = acts(cfg)
     ks = list(range(cfg["bank_scale"], cfg["bank_size"] + 1, cfg["bank_scale"]))
     outs = [relu(pad_conv(x, w(f"{p}conv_bank.{i}.weight"), w(f"{p}conv_bank.{i}.bias")))
@@ -241,7 +242,10 @@ def ce_forward(w, cfg, x, p="content_encoder."):
         if s > 1:
             out = avg_pool_ceil(out, s)
         out = y + out
-    return pad_conv(out, w(p + "mean_layer.weight"), w(p + "mean_layer.bias"))
+    mu = pad_conv(out, w(p + "mean_layer.weight"), w(p + "mean_layer.bias"))
+    if log_sigma:
+        return mu, pad_conv(out, w(p + "std_layer.weight"), w(p + "std_layer.bias"))
+    return mu
 
 
 def pixel_shuffle_1d(x, s):

@@ -290,3 +290,49 @@ def test_pgd_restatement_properties(golden):
     e0, _ = oracle.se_forward(w, se, z["vc_tgt"] + 0.1 * np.tanh(z["emb_ptb0"]))
     e1, _ = oracle.se_forward(w, se, adv)
     assert ((e1 - tgt) ** 2).mean() < ((e0 - tgt) ** 2).mean()
+
+
+def test_module_forwards_oracle(golden):
+    """ContentEncoder.forward (mu, log_sigma), Decoder.forward and the PredictiveModel block chain
+    of the reference (tests/golden/modules.npz, make_modules.py) reproduced by the restatements."""
+    from oracle import predictive as po
+    zm = golden("modules")
+    hs = json.loads(str(zm["weight_sha256"]))
+    torch.manual_seed(0)
+    m = models.AdaInVC(cfg_of(zm))
+    for k, v in m.state_dict().items():
+        assert hashlib.sha256(v.numpy().tobytes()).hexdigest() == hs[k], k
+    w = oracle_weights(m)
+    cfg = cfg_of(zm)
+    for T in (128, 300):
+        mu, ls = oracle.ce_forward(w, cfg["ContentEncoder"], zm[f"ce_x_T{T}"], log_sigma=True)
+        assert rel(mu, zm[f"ce_mu_T{T}"]) <= 1e-5 and rel(ls, zm[f"ce_log_sigma_T{T}"]) <= 1e-5
+    for Tz in (16, 37):
+        out = oracle.dec_forward(w, cfg["Decoder"], zm[f"dec_z_T{Tz}"], zm[f"dec_cond_T{Tz}"])
+        assert rel(out, zm[f"dec_out_T{Tz}"]) <= 1e-5
+    zp = golden("predictive")
+    import predictive_model
+    torch.manual_seed(0)
+    pm = predictive_model.PredictiveModel()
+    sd = {k: v.numpy().copy() for k, v in pm.state_dict().items()}
+    for k in zp:
+        if k.startswith("p/"):
+            sd[k[2:]] = zp[k]
+    # block by block, each fed the reference's output of the previous block: a block's own
+    # numerics only (chained, an isolated PReLU / LeakyReLU sign flip at a near-zero
+    # pre-activation amplifies through the later blocks)
+    h = zm["pm_x"]
+    for i, (_, _, st) in enumerate(po.DOWN):
+        p = f"down_blocks.{i}.conv."
+        y = po.conv2d_reflect(h, sd[p + "1.weight"], sd[p + "1.bias"], st)
+        sc = sd[p + "2.weight"] / np.sqrt(sd[p + "2.running_var"] + np.float32(1e-5))
+        y = (y - sd[p + "2.running_mean"][None, :, None, None]) * sc[None, :, None, None] + sd[p + "2.bias"][None, :, None, None]
+        y = np.where(y >= 0, y, sd[p + "3.weight"][0] * y)
+        assert rel(y, zm[f"pm_down{i}"]) <= 1e-5, (i, rel(y, zm[f"pm_down{i}"]))
+        h = zm[f"pm_down{i}"]
+    for i in range(len(po.UP)):
+        p = f"up_blocks.{i}.conv_transpose.0."
+        y = po.conv_transpose2d(h, sd[p + "weight"], sd[p + "bias"])
+        y = np.where(y >= 0, y, np.float32(0.2) * y)
+        assert rel(y, zm[f"pm_up{i}"]) <= 1e-5, (i, rel(y, zm[f"pm_up{i}"]))
+        h = zm[f"pm_up{i}"]
