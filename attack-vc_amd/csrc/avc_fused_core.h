@@ -323,12 +323,15 @@ __device__ __forceinline__ void fz_gemm_res(f32x4 (&acc)[MT][NF], IC<NFC>, const
 // Diagnostic build only (-DAVC_FZ_PHASES): per-wave cycle stamps at phase boundaries,
 // printed by workgroup 0 at the end of the kernel (scripts/dbg/phases.sh).
 #ifdef AVC_FZ_PHASES
+#ifndef FZ_PH_MAX
+#define FZ_PH_MAX 96
+#endif
 #define FZ_PH_DECL          \
-    unsigned long long fz_ph[96]; \
+    unsigned long long fz_ph[FZ_PH_MAX]; \
     int fz_phn = 0;
 #define FZ_PH()                                                            \
     do {                                                                   \
-        if (fz_phn < 96) fz_ph[fz_phn++] = __builtin_readcyclecounter();   \
+        if (fz_phn < FZ_PH_MAX) fz_ph[fz_phn++] = __builtin_readcyclecounter();   \
     } while (0)
 #define FZ_PH_DUMP(tag)                                                                            \
     do {                                                                                           \

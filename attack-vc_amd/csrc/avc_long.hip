@@ -319,6 +319,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
     const bool ce = A.ce_mode != 0;
     const bool wm = A.write_masks != 0 && !ce;
     if (A.tick && b == 0 && tid == 0) atomicAdd(A.tick, 1);
+    FZ_PH_DECL
+    FZ_PH();
 
     char* imgx = L.img[0] + (size_t)b * L.img_stride;
     char* imgh = L.img[1] + (size_t)b * L.img_stride;
@@ -366,6 +368,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         }
     }
     lz_publish();
+    FZ_PH();
 
     int rb[NF];
     f32x4 in_s[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // ContentEncoder: IN row sums
@@ -386,6 +389,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             __syncthreads();                             // the previous chunk's readers are done
             lz_stage<PREC>(XB, imgx, LZ_ZR + n0 - 4, NXR);
             __syncthreads();
+            FZ_PH();
             f32x4 acc_h[2][NF];
             zero_acc(acc_h);
             auto bank_step = [&](auto KB) __attribute__((always_inline)) {
@@ -419,9 +423,11 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                 if (!DBUF) __syncthreads();
             };
             for (int kb = 0; kb < nb; ++kb) bank_step(kb);
+            FZ_PH();
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T - 1) - n0 + 4;
             fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc_h, IC<NF>{}, ring, op_inx(), chk.last ? op_c1(0) : op_bank(0), XB, rb);
+            FZ_PH();
             // h0 = act(in_conv + b) (SpeakerEncoder) / raw in_conv + b (ContentEncoder: IN next)
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
@@ -447,6 +453,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                         }
                     }
             }
+            FZ_PH();
         }
     }
     // ContentEncoder: h0 = act(IN(in_conv + b)) (models.py:195-200)
@@ -487,6 +494,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             bc2[i] = *reinterpret_cast<const f32x4*>(A.w.b_c2[l] + ch0 + 16 * i);
         }
         lz_publish();                                   // imgh of this block complete
+        FZ_PH();
         // conv1 (stride 1): y1 = act(conv1(h) + b1)
         LzChunk chk;
         const int nfi = lz_nf(Ti);
@@ -497,11 +505,13 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
             const char* SB = pipe1.next(k, chk, imgh, r0_c1, nr_c1);
+            FZ_PH();
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Ti - 1) - n0;
             f32x4 acc[2][NF];
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c1(l), chk.last ? op_c2(l) : op_c1(l), SB, rb);
+            FZ_PH();
             pipe1.issue_next(k, imgh, r0_c1, nr_c1);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
@@ -526,12 +536,14 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                         }
                     }
             }
+            FZ_PH();
         }
         if (ce)
             in_apply(Ti, [&](int t, int i, f32x4 v) __attribute__((always_inline)) {
                 lz_put<PREC>(imgy, t, Ti, (ch0 + 16 * i) * ESZ, v);
             });
         lz_publish();                                   // imgy complete
+        FZ_PH();
         // conv2 (stride s): y2 = act(conv2(y1) + b2); h = y2 + avg_pool1d(h, s, ceil_mode)
         float* hin = hf[cur];
         float* hout = hf[cur ^ 1];
@@ -549,12 +561,14 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         for (int k = 0; lz_chunk(k, nfo, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
             const char* SB = pipe2.next(k, chk, imgy, r0_c2, nr_c2);
+            FZ_PH();
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = s * (min(n0 + 16 * f + c, To - 1) - n0);
             f32x4 acc[2][NF];
             zero_acc(acc);
             const AOp nxt = chk.last ? (!lastblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l))) : op_c2(l);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l), nxt, SB, rb);
+            FZ_PH();
             pipe2.issue_next(k, imgy, r0_c2, nr_c2);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
@@ -582,6 +596,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                         }
                     }
             }
+            FZ_PH();
         }
         if (ce)
             in_apply(To, [&](int t, int i, f32x4 v) __attribute__((always_inline)) {
@@ -635,6 +650,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             *reinterpret_cast<f32x4*>(A.pooled + (size_t)b * FZ_C + ch0 + 16 * i) = m;
         }
     }
+    FZ_PH();
+    FZ_PH_DUMP("lfwd");
 }
 
 // ---------------------------------------------------------------------------------
@@ -671,6 +688,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         return mk + ((size_t)(layer * L.nFmax + F) * 4 + w) * 8;
     };
     float* FSCR = reinterpret_cast<float*>(fz_lds + 150 * 1024) + w * (5 * 16 * 8);
+    FZ_PH_DECL
+    FZ_PH();
 
     const int ns_c = ks * FZ_C / KS;
     auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
@@ -724,6 +743,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         lz_zero_rows<PREC>(imgg, 0, LZ_ZR);
         lz_zero_rows<PREC>(imgg, LZ_ZR + s * To, LZ_ZR);
         lz_publish();
+        FZ_PH();
         // conv2^T over padded positions v = n - 16 of the Ti input frames, * act'(y1) -> imgg2
         const int nfc = lz_nf(Ti + 16 + P);
         LzChunk chk;
@@ -740,6 +760,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             const int n0 = 16 * chk.f0;
             const int r0 = r0_g(chk);
             const char* SB = pipeg.next(k, chk, imgg, r0_g, nr_g);
+            FZ_PH();
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
@@ -748,6 +769,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             f32x4 acc[2][NF];
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c2T(l), chk.last ? op_c1T(l) : op_c2T(l), SB, rb);
+            FZ_PH();
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
             pipeg.issue_next(k, imgg, r0_g, nr_g);
 #pragma unroll
@@ -765,10 +787,12 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                         st4<PREC>(imgg2 + (size_t)(LZ_ZR + t) * GRB + (ch0 + 16 * i) * ESZ, v);
                     }
             }
+            FZ_PH();
         }
         lz_zero_rows<PREC>(imgg2, 0, LZ_ZR);
         lz_zero_rows<PREC>(imgg2, LZ_ZR + Ti, LZ_ZR);
         lz_publish();
+        FZ_PH();
         // conv1^T (+ fold) + avg_pool^T of g(h_{l+1}) -> g(h_l); then the next dY: the dilated
         // dY2 of block l-1 = g(h_l) * act'(y2_{l-1}), or g_pre0 = g(h_0) * act'(h0)
         const int sp = l > 0 ? A.sub[l - 1] : 1;
@@ -782,6 +806,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             const int n0 = 16 * chk.f0;
             const int r0 = r0_g(chk);
             const char* SB = pipeg2.next(k, chk, imgg2, r0_g, nr_g);
+            FZ_PH();
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
@@ -796,6 +821,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             } else {
                 fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), nxt, SB, rb);
             }
+            FZ_PH();
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
             pipeg2.issue_next(k, imgg2, r0_g, nr_g);
 #pragma unroll
@@ -827,6 +853,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                                       f32x4{0.f, 0.f, 0.f, 0.f});
                     }
             }
+            FZ_PH();
         }
         cur ^= 1;
     }
@@ -844,6 +871,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     lz_zero_rows<PREC>(imgp, 0, LZ_ZR);
     lz_zero_rows<PREC>(imgp, LZ_ZR + T, LZ_ZR);
     lz_publish();
+    FZ_PH();
     char* GP = fz_lds;                                  // g_pre0 rows of frames n0-16 .. n0+CH-1
     char* GBK = GP + NFW * 16 * RS;                     // per-wave g(b_k) slices, ZPB + NFW*16 + ZPB rows
     static_assert((NFW * 16 + NFW * 16 + 2 * ZPB) * RS <= 150 * 1024, "bank windows overlap the fold scratch");
@@ -876,6 +904,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             }
         }
         __syncthreads();
+        FZ_PH();
         f32x4 accx[5][LZ_CHF];
         zero_acc(accx);
         // x passthrough of the cat: W_in[:, x block]^T g_pre0.  Pad columns read g_pre0 rows of
@@ -929,11 +958,14 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             }
             asm volatile("" ::: "memory");   // (the next gate rewrites this wave's slice: in order)
         };
+        FZ_PH();
         for (int kb = 0; kb < nb; ++kb) bank_step(kb);
+        FZ_PH();
         if (!chk.last) {   // ring5 now holds op_bankT(nb-1) prefetches; the next chunk starts at in_x^T
             ring_fill(ring5, op_inTx());
         }
         lz_fold<5, CHF>(accx, chk.f0, 4, T, 4, FSCR);
+        FZ_PH();
         // deterministic cross-wave sum ((p0 + p2) + (p1 + p3)) into R0 / R1 [80][CH]
         for (int phase = 0; phase < 2; ++phase) {
             if ((phase == 0) == (w >= 2)) {
@@ -950,6 +982,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             }
             __syncthreads();
         }
+        FZ_PH();
         // owned interior columns: t = n - 4 in [0, T).  UB elements per thread per batch, all
         // their state loads issued before any arithmetic (one memory round trip per batch; 20:
         // two round trips per 128-column chunk instead of ten)
@@ -990,7 +1023,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                 Ad.adv[q] = ad;
             }
         }
+        FZ_PH();
     }
+    FZ_PH_DUMP("lbwd");
 }
 
 // ---------------------------------------------------------------------------------
