@@ -116,6 +116,11 @@ SIGNATURES = [
                                         ctypes.POINTER(ctypes.c_int)]),
     ("avc_pm_forward", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_pm_block_shape", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_int)]),
+    ("avc_pm_block_forward", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_vsmask_windows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     ("avc_vsmask_protect", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
@@ -635,6 +640,23 @@ class PMContext:
         with self._lock:
             _check(lib().avc_pm_forward(self.h, ctypes.c_void_p(x.data_ptr()), B, H, W,
                                         ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(stream)))
+        return y
+
+    def block_forward(self, layer: int, x: torch.Tensor) -> torch.Tensor:
+        """One block: layer 0..6 = down_blocks.i, 7..11 = up_blocks.(i-7) (avc_pm_block_forward)."""
+        _require_gpu(x)
+        x = x.contiguous()
+        if x.dim() != 4:
+            raise RuntimeError(f"expected [B, C, H, W], got {tuple(x.shape)}")
+        B, C, H, W = x.shape
+        c, ho, wo = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().avc_pm_block_shape(self.h, int(layer), int(H), int(W), ctypes.byref(c), ctypes.byref(ho),
+                                        ctypes.byref(wo)))
+        y = torch.empty(B, c.value, ho.value, wo.value, device=x.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        with self._lock:
+            _check(lib().avc_pm_block_forward(self.h, int(layer), ctypes.c_void_p(x.data_ptr()), B, H, W,
+                                              ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(stream)))
         return y
 
     def protect(self, mel: torch.Tensor, header: Optional[torch.Tensor], window_size: int = 100,

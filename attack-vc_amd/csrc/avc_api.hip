@@ -50,6 +50,8 @@ __global__ void hdr_compose(HdrArgs A);
 __global__ void hdr_update(HdrArgs A);
 __global__ void pm_conv(PmConvArgs P);
 __global__ void pm_reduce(PmConvArgs P);
+template <int MT>
+__global__ void pm_mfma(PmConvArgs P);
 __global__ void vsm_gather(VsmArgs A);
 __global__ void vsm_combine(VsmArgs A);
 }  // namespace avc

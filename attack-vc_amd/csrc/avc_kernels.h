@@ -279,6 +279,9 @@ struct PmConvArgs {
     int32_t woff[4];
     int32_t ksplit;                   // > 1: K slices (blockIdx.z = class * ksplit + slice) write raw
     float* part;                      //      partial sums to part[slice][B*Cout*Ho*Wo]; pm_reduce finishes
+    int32_t in_nhwc, out_nhwc;        // activation layouts (pm_conv): 0 = NCHW, 1 = NHWC (pm_mfma: both NHWC)
+    const float* wm;                  // pm_mfma: A in MFMA fragment order, class c at wmoff[c] floats:
+    int32_t wmoff[4];                 //   [m tile][K chunk of 16][64 lanes][4], K = (tap, ci)
 };
 
 // DSP frame kernels (avc_dsp.hip): LDS slot of complex element i of the FFT buffer,

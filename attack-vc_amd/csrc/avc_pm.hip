@@ -19,6 +19,8 @@
 
 namespace avc {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float pm_act(float v, const PmConvArgs& P) {
     if (P.act == 0) return v >= 0.f ? v : P.slope * v;                // PReLU
     v = v >= 0.f ? v : 0.2f * v;                                      // LeakyReLU(0.2)
@@ -87,7 +89,7 @@ __global__ void __launch_bounds__(256) pm_conv(PmConvArgs P) {
                     ix = px == 0 ? qx - bb : qx;
                     ok = iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
                 }
-                if (ok) v = xb[((size_t)ci * P.Hin + iy) * P.Win + ix];
+                if (ok) v = P.in_nhwc ? xb[((size_t)iy * P.Win + ix) * P.Cin + ci] : xb[((size_t)ci * P.Hin + iy) * P.Win + ix];
             }
             rb[j] = v;
         }
@@ -141,7 +143,8 @@ __global__ void __launch_bounds__(256) pm_conv(PmConvArgs P) {
         for (int i = 0; i < 4; ++i) {
             const int co = m0 + 4 * ty + i;
             if (co >= P.Cout) continue;
-            const size_t o = (((size_t)ob * P.Cout + co) * P.Ho + oy) * P.Wo + ox;
+            const size_t o = P.out_nhwc ? (((size_t)ob * P.Ho + oy) * P.Wo + ox) * P.Cout + co
+                                        : (((size_t)ob * P.Cout + co) * P.Ho + oy) * P.Wo + ox;
             if (ks > 1) P.part[(size_t)slice * per + o] = acc[i][j];
             else P.y[o] = pm_act(acc[i][j] + P.bias[co], P);
         }
@@ -155,9 +158,141 @@ __global__ void __launch_bounds__(256) pm_reduce(PmConvArgs P) {
     if (o >= per) return;
     float s = 0.f;
     for (int q = 0; q < P.ksplit; ++q) s += P.part[(size_t)q * per + o];
-    const int co = (int)((o / ((size_t)P.Ho * P.Wo)) % P.Cout);
+    const int co = P.out_nhwc ? (int)(o % P.Cout) : (int)((o / ((size_t)P.Ho * P.Wo)) % P.Cout);
     P.y[o] = pm_act(s + P.bias[co], P);
 }
+
+// ---------------------------------------------------------------------------------
+// The same layers on the matrix cores: v_mfma_f32_16x16x4_f32 (exact fp32, the fp32 peak).
+// Activations NHWC, K ordered (tap, input channel) with Cin % 16 == 0, so one 16-wide K chunk
+// is ONE input pixel's 16 consecutive channels: a lane's B fragment (column = output pixel,
+// 4 consecutive K) is one 16-byte load, and the reflect (mode 0) / parity-class (mode 1) index
+// arithmetic runs once per tap, not per element.  A comes pre-packed in fragment order (one
+// 16-byte load per lane per M tile per chunk).  Within a chunk the four MFMA steps take K
+// values 4q + s of lane group q (a permutation of the chunk, applied to A and B alike).
+// Workgroup: 4 waves side by side over N, each MT x 16 rows by 32 columns (two N tiles); no
+// LDS -- A is shared by the 4 waves through L1, B by the M tiles of a wave in registers.  The
+// next chunk's fragments are in flight during the current chunk's MFMAs.  Per output the
+// summation order is fixed by the layer's (geometry-only) K split: batch-invariant.
+// ---------------------------------------------------------------------------------
+template <int MT>
+__global__ void __launch_bounds__(256) pm_mfma(PmConvArgs P) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 15, q = lane >> 4;
+    const int ks = P.ksplit > 1 ? P.ksplit : 1;
+    const int cls = blockIdx.z / ks, slice = blockIdx.z - cls * ks;
+    const int py = cls >> 1, px = cls & 1;
+    const int nty = P.mode == 1 ? (py == 0 ? 2 : 1) : 3;
+    const int ntx = P.mode == 1 ? (px == 0 ? 2 : 1) : 3;
+    const int Hq = P.mode == 1 ? (P.Ho - py + 1) / 2 : P.Ho;
+    const int Wq = P.mode == 1 ? (P.Wo - px + 1) / 2 : P.Wo;
+    const int N = P.B * Hq * Wq;
+    const int nbase = blockIdx.x * 128;
+    if (nbase >= N) return;                     // (uniform: class grids are padded to the largest)
+    const int ccpt = P.Cin >> 4;                // K chunks per tap
+    const int nchunk = nty * ntx * ccpt;
+    const int cps = (nchunk + ks - 1) / ks;
+    const int kc0 = slice * cps, kc1 = min(nchunk, kc0 + cps);
+    const int mt0 = blockIdx.y * MT;            // first M tile of this workgroup
+    const int nmt = (P.Cout + 15) >> 4;
+    // this lane's two output columns
+    int cb[2], cy[2], cx[2];
+    bool cv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = nbase + 32 * w + 16 * j + c;
+        cv[j] = n < N;
+        const int nn = cv[j] ? n : 0;
+        cb[j] = nn / (Hq * Wq);
+        const int r = nn - cb[j] * Hq * Wq;
+        cy[j] = r / Wq;
+        cx[j] = r - cy[j] * Wq;
+    }
+    const f32x4* __restrict__ Aw = reinterpret_cast<const f32x4*>(P.wm + P.wmoff[cls]);
+    auto load_a = [&](int kc, f32x4 (&a)[MT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int mt = min(mt0 + i, nmt - 1);
+            a[i] = Aw[((size_t)mt * nchunk + kc) * 64 + lane];
+        }
+    };
+    auto load_b = [&](int kc, f32x4 (&b)[2]) __attribute__((always_inline)) {
+        const int tap = kc / ccpt, ci = ((kc - tap * ccpt) << 4) + 4 * q;
+        const int a = tap / ntx, bb = tap - a * ntx;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            int iy, ix;
+            bool ok = cv[j];
+            if (P.mode == 0) {
+                iy = cy[j] * P.sh + a - 1;
+                ix = cx[j] * P.sw + bb - 1;
+                iy = iy < 0 ? -iy : (iy >= P.Hin ? 2 * (P.Hin - 1) - iy : iy);
+                ix = ix < 0 ? -ix : (ix >= P.Win ? 2 * (P.Win - 1) - ix : ix);
+            } else {
+                iy = py == 0 ? cy[j] - a : cy[j];
+                ix = px == 0 ? cx[j] - bb : cx[j];
+                ok = ok && iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
+            }
+            b[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (ok) b[j] = *reinterpret_cast<const f32x4*>(P.x + (((size_t)cb[j] * P.Hin + iy) * P.Win + ix) * P.Cin + ci);
+        }
+    };
+    f32x4 acc[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 a0[MT], a1[MT], b0[2], b1[2];
+    auto mma = [&](const f32x4 (&a)[MT], const f32x4 (&b)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+    };
+    if (kc0 < kc1) {
+        load_a(kc0, a0);
+        load_b(kc0, b0);
+    }
+    int kc = kc0;
+    for (; kc + 1 < kc1; kc += 2) {
+        load_a(kc + 1, a1);
+        load_b(kc + 1, b1);
+        mma(a0, b0);
+        if (kc + 2 < kc1) {
+            load_a(kc + 2, a0);
+            load_b(kc + 2, b0);
+        }
+        mma(a1, b1);
+    }
+    if (kc < kc1) mma(a0, b0);
+    // epilogue: rows 4q + r of M tile i = 4 consecutive output channels of column (j, c): NHWC
+    const size_t per = (size_t)P.B * P.Cout * P.Ho * P.Wo;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!cv[j]) continue;
+        const int oy = P.mode == 1 ? 2 * cy[j] + py : cy[j];
+        const int ox = P.mode == 1 ? 2 * cx[j] + px : cx[j];
+        const size_t pix = ((size_t)cb[j] * P.Ho + oy) * P.Wo + ox;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int co = (mt0 + i) * 16 + 4 * q;
+            if (co >= P.Cout) continue;
+            const size_t o = pix * P.Cout + co;
+            if (ks > 1) {
+                *reinterpret_cast<f32x4*>(P.part + (size_t)slice * per + o) = acc[i][j];
+            } else {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = pm_act(acc[i][j][r] + P.bias[co + r], P);
+                *reinterpret_cast<f32x4*>(P.y + o) = v;
+            }
+        }
+    }
+}
+template __global__ void pm_mfma<2>(PmConvArgs);
+template __global__ void pm_mfma<4>(PmConvArgs);
 
 // ---- VSMask protect loop (/root/reference/vsmask.py:177-208) ----------------------------
 // The reference walks start = 0, S, 2S, ... < T - W, feeds mel[..., start:start+W] (always the

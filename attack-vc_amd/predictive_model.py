@@ -5,14 +5,34 @@ draws the reference's default-init weights -- whose forward runs on the MI355X t
 libavc's HIP kernels (csrc/avc_pm.hip), eval-mode semantics (BatchNorm running
 statistics), no autograd.
 """
+import weakref
 from typing import Tuple
 
 import torch
 import torch.nn as nn
 
 
-class DownSamplingBlock(nn.Module):
-    """predictive_model.py:6-29: ReflectionPad2d -> Conv2d -> BatchNorm2d -> PReLU."""
+class _Block:
+    """A block's forward runs on libavc through the PredictiveModel it belongs to (its weights are
+    uploaded with the whole network's): weak back-reference + its layer index."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        ref = self.__dict__.get("_avc_parent")
+        m = ref() if ref is not None else None
+        if m is None:
+            raise RuntimeError(f"{type(self).__name__}.forward runs on libavc through the PredictiveModel it belongs "
+                               "to; build it inside PredictiveModel")
+        from avc_native import pm_context_for
+        return pm_context_for(m, x.device).block_forward(self.__dict__["_avc_layer"], x.float())
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st.pop("_avc_parent", None)
+        return st
+
+
+class DownSamplingBlock(_Block, nn.Module):
+    """predictive_model.py:6-29: ReflectionPad2d -> Conv2d -> BatchNorm2d -> PReLU (eval semantics)."""
 
     def __init__(self, in_channels: int, out_channels: int, kernel_size: Tuple[int, int], stride: Tuple[int, int]):
         super().__init__()
@@ -23,7 +43,7 @@ class DownSamplingBlock(nn.Module):
             nn.PReLU())
 
 
-class UpSamplingBlock(nn.Module):
+class UpSamplingBlock(_Block, nn.Module):
     """predictive_model.py:31-51: ConvTranspose2d -> LeakyReLU(0.2)."""
 
     def __init__(self, in_channels: int, out_channels: int, kernel_size: Tuple[int, int], stride: Tuple[int, int]):
@@ -52,6 +72,16 @@ class PredictiveModel(nn.Module):
             UpSamplingBlock(64, 32, (3, 3), (2, 2)),
             UpSamplingBlock(32, 1, (3, 3), (2, 2))])
         self.tanh = nn.Tanh()
+        self._avc_link()
+
+    def _avc_link(self):
+        for i, blk in enumerate(list(self.down_blocks) + list(self.up_blocks)):
+            object.__setattr__(blk, "_avc_parent", weakref.ref(self))
+            object.__setattr__(blk, "_avc_layer", i)
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        self._avc_link()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         from avc_native import predictive_forward

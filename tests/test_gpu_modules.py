@@ -62,3 +62,34 @@ def test_standalone_module_refuses():
 def models_cfg():
     import bench
     return bench.FULL_CFG
+
+
+def test_predictive_blocks_forward(golden):
+    """DownSamplingBlock / UpSamplingBlock.forward (models/predictive_model.py:28-29, 50-51) of the
+    reference's PredictiveModel (weights of tests/golden/predictive.npz), each block fed the
+    reference's output of the previous one; the chain of blocks + tanh equals the whole forward."""
+    import predictive_model
+    zm, zp = golden("modules"), golden("predictive")
+    torch.manual_seed(0)
+    pm = predictive_model.PredictiveModel()
+    sd = pm.state_dict()
+    for k in zp:
+        if k.startswith("p/"):
+            sd[k[2:]] = torch.from_numpy(zp[k])
+    pm.load_state_dict(sd)
+    pm = pm.eval().to(DEV)
+    h = zm["pm_x"]
+    names = [f"pm_down{i}" for i in range(7)] + [f"pm_up{i}" for i in range(5)]
+    blocks = list(pm.down_blocks) + list(pm.up_blocks)
+    for blk, name in zip(blocks, names):
+        y = blk(_dev(h)).cpu().numpy()
+        assert y.shape == zm[name].shape, name
+        assert rel(y, zm[name]) <= 1e-5, (name, rel(y, zm[name]))
+        h = zm[name]
+    x = _dev(zm["pm_x"])
+    chain = x
+    for blk in blocks:
+        chain = blk(chain)
+    full = pm(x)
+    assert full.shape == chain.shape
+    assert float((torch.tanh(chain) - full).abs().max()) <= 1e-4
