@@ -33,6 +33,10 @@ __global__ void se_fwd_fused(FusedArgs A);
 template <int PREC, int SH>
 __global__ void se_bwd_fused(FusedArgs A);
 template <int PREC>
+__global__ void se_fwd8(FusedArgs A);
+template <int PREC>
+__global__ void se_bwd8(FusedArgs A);
+template <int PREC>
 __global__ void lz_se_fwd(FusedArgs A, LongArgs L);
 template <int PREC>
 __global__ void lz_se_bwd(FusedArgs A, LongArgs L);
@@ -133,6 +137,7 @@ struct Launch {
     FusedArgs fz{};              // L_FZ_* / L_LZ_*: per-utterance SpeakerEncoder pass (prec = PREC_*)
     LongArgs lz{};               // L_LZ_*: the long engine's scratch
     int fz_shape = 8;            // L_FZ_*: kernel shape SH (0 = standard config at T = 128, else 1|2|4|8)
+    bool fz8 = false;            // L_FZ_* bf16 shape 0: the 8-wave kernels (avc_fused8.hip)
     DecArgs dz{};                // L_DZ_*: per-utterance fused Decoder pass (shape: fz_shape 0 | 8)
     DenseArgs dn{};              // L_DENSE: batched conv_affine layer (or its transpose)
     HdrArgs hd{};                // L_HDR_*: the header optimiser's elementwise ends
@@ -456,6 +461,10 @@ static int set_fused_attrs() {
                                                AVC_FZ_FNS(8)};
 #undef AVC_FZ_FNS
     for (auto& fn : fns) HIPCHK(hipFuncSetAttribute(fn.first, hipFuncAttributeMaxDynamicSharedMemorySize, fn.second));
+    HIPCHK(hipFuncSetAttribute((const void*)se_fwd8<PREC_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               fz_max2(fz8_lds_fwd(128, 5), (4 * 6 + 8) * FZ_C * (int)sizeof(float))));
+    HIPCHK(hipFuncSetAttribute((const void*)se_bwd8<PREC_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               fz8_lds_bwd(128)));
     for (const void* fn : {(const void*)lz_se_fwd<PREC_F32>, (const void*)lz_se_fwd<PREC_BF16>,
                            (const void*)lz_se_bwd<PREC_F32>, (const void*)lz_se_bwd<PREC_BF16>,
                            (const void*)lz_dec_fwd<PREC_F32>, (const void*)lz_dec_fwd<PREC_BF16>,
@@ -1151,6 +1160,18 @@ static int fused_shape(avc_ctx* ctx, int T) {
     return nf <= 1 ? 1 : nf <= 2 ? 2 : nf <= 4 ? 4 : 8;
 }
 
+// AVC_FZ8=1: bf16 passes of the standard shape on the 8-wave kernels (two waves per SIMD, bitwise
+// the 4-wave results).  Opt-in: measured slower than the 4-wave engine
+static void use_fz8(Launch& L) {
+    if ((L.kind != L_FZ_FWD && L.kind != L_FZ_BWD) || L.prec != PREC_BF16 || L.fz_shape != 0 || L.fz.T != 128) return;
+    const char* e = getenv("AVC_FZ8");
+    if (!(e && e[0] == '1')) return;
+    L.fz8 = true;
+    L.block = dim3(512);
+    L.shmem = std::max(L.shmem, (size_t)(L.kind == L_FZ_FWD ? fz8_lds_fwd(128, 5) : fz8_lds_bwd(128)));
+    L.name = L.kind == L_FZ_FWD ? "se_fwd8<bf16>" : "se_bwd8<bf16>";
+}
+
 static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, bool attack, int prec) {
     const avc_se_cfg& c = ctx->cfg;
     const int B = ws.B;
@@ -1219,9 +1240,11 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
         F.fz.loss_cur = ws.loss_cur.p;
         F.flop += L.flop;
         F.name = "se_fwd_fused<bf16>";
+        use_fz8(F);
         pl.launches.push_back(F);
         return 0;
     }
+    use_fz8(F);
     pl.launches.push_back(F);
     pl.launches.push_back(L);
     return 0;
@@ -1252,6 +1275,7 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
     L.flop = fz_fwd_flop(ctx->cfg, ws.Tl, ctx->bank_k) * ws.B;   // input-gradient only
     L.name = prec == PREC_F32 ? "se_bwd_fused<f32>" : "se_bwd_fused<bf16>";
     if (ws.lz) L.name = prec == PREC_F32 ? "lz_se_bwd<f32>" : "lz_se_bwd<bf16>";
+    use_fz8(L);
     pl.launches.push_back(L);
     return 0;
 }
@@ -1528,6 +1552,11 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
                       : L.fz_shape == 4 ? AVC_FZ_K(4)
                                         : AVC_FZ_K(8);
 #undef AVC_FZ_K
+        if (L.fz8) {
+            if (L.kind == L_FZ_FWD) klaunch(ev, false, se_fwd8<PREC_BF16>, L.grid, L.block, L.shmem, s, L.fz);
+            else klaunch(ev, false, se_bwd8<PREC_BF16>, L.grid, L.block, L.shmem, s, L.fz);
+            return hipGetLastError();
+        }
         klaunch(ev, false, k, L.grid, L.block, L.shmem, s, L.fz);
         return hipGetLastError();
     }

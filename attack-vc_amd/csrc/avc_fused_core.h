@@ -124,7 +124,7 @@ __device__ __forceinline__ const f32x4* a_step(const AOp& o, int s) {
 // load -> wait -> use on every step)
 template <int MTR, int RD = 4>
 struct ARing {
-    static_assert(RD == 2 || RD == 4, "ring depth");
+    static_assert(RD == 2 || RD == 4 || RD == 8, "ring depth");
     f32x4 a[RD][MTR];
 };
 // slot <- step s of A (s < A.ns) or step s - A.ns of N; branch-free (uniform selects);
@@ -198,21 +198,28 @@ __device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing
     f32x4 bA[NL], bB[NL];
     read_b(bA, 0);
     const int nfull = ns & ~(RD - 1);
+    // slot u of an iteration: B of step s+u+1 into the idle buffer, MFMAs of step s+u, then the
+    // slot refilled with step s+u+RD
 #pragma unroll 1
     for (int s = 0; s < nfull; s += RD) {
-        read_b(bB, s + 1);
-        mma_all(R.a[0], bA);
-        ring_load<MTR>(R.a[0], A, N, s + RD);
-        read_b(bA, s + 2);
-        mma_all(R.a[1], bB);
-        ring_load<MTR>(R.a[1], A, N, s + RD + 1);
-        if constexpr (RD == 4) {
-            read_b(bB, s + 3);
-            mma_all(R.a[2], bA);
-            ring_load<MTR>(R.a[2], A, N, s + 6);
-            read_b(bA, s + 4);
-            mma_all(R.a[3], bB);
-            ring_load<MTR>(R.a[3], A, N, s + 7);
+#pragma unroll
+        for (int u = 0; u < RD; ++u) {
+            if (u & 1) {
+                read_b(bA, s + u + 1);
+                mma_all(R.a[u], bB);
+            } else {
+                read_b(bB, s + u + 1);
+                mma_all(R.a[u], bA);
+            }
+            ring_load<MTR>(R.a[u], A, N, s + RD + u);
+#if !(AVC_FZ_ABLATE & 8) && !defined(AVC_FZ_RING_FREE)
+            // keep each refill in its own step: left alone, the scheduler sinks all RD refills to
+            // the end of the iteration (the loaded registers are consumed a whole iteration
+            // later, so the refills look like the least critical work), and the first MFMAs of
+            // the next iteration then wait for an L2 round trip -- the ring's prefetch collapses
+            // (AVC_FZ_RING_FREE: the long engine, whose chunked GEMMs measured 3 % faster without)
+            __builtin_amdgcn_sched_barrier(0);
+#endif
         }
     }
     // remainder (0..RD-1 steps): slots hold steps nfull..nfull+RD-1 (slot u = step nfull+u),
@@ -220,46 +227,35 @@ __device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing
     const int rem = ns - nfull;
 #if AVC_FZ_ABLATE & 4
     // debug: no cross-GEMM prefetch -- finish this GEMM's own steps, then load N afresh
-    if (rem >= 1) mma_all(R.a[0], bA);
-    if constexpr (RD == 4) {
-        if (rem >= 2) {
-            read_b(bB, nfull + 1);
-            mma_all(R.a[1], bB);
+#pragma unroll
+    for (int u = 0; u < RD - 1; ++u)
+        if (u < rem) {
+            if (u & 1) read_b(bB, nfull + u);
+            else if (u) read_b(bA, nfull + u);
+            mma_all(R.a[u], (u & 1) ? bB : bA);
         }
-        if (rem >= 3) {
-            read_b(bA, nfull + 2);
-            mma_all(R.a[2], bA);
-        }
-    }
     ring_fill(R, N);
     return;
 #endif
     if (rem == 0) return;
-    mma_all(R.a[0], bA);
-    ring_load<MTR>(R.a[0], A, N, nfull + RD);
-    if constexpr (RD == 4) {
-        if (rem >= 2) {
-            read_b(bB, nfull + 1);
-            mma_all(R.a[1], bB);
-            ring_load<MTR>(R.a[1], A, N, nfull + 5);
+#pragma unroll
+    for (int u = 0; u < RD - 1; ++u)
+        if (u < rem) {
+            if (u & 1) read_b(bB, nfull + u);
+            else if (u) read_b(bA, nfull + u);
+            mma_all(R.a[u], (u & 1) ? bB : bA);
+            ring_load<MTR>(R.a[u], A, N, nfull + RD + u);
         }
-        if (rem >= 3) {
-            read_b(bA, nfull + 2);
-            mma_all(R.a[2], bA);
-            ring_load<MTR>(R.a[2], A, N, nfull + 6);
-        }
-    }
     // a GEMM shorter than the ring (ns < RD) entered with slots u >= ns holding clamped
     // copies of its own last step (its predecessor could not know this GEMM's successor):
     // those slots get N's steps u - rem now
     if (nfull == 0)
-        for (int u = rem; u < RD; ++u) {
 #pragma unroll
-            for (int v = 0; v < RD; ++v)
-                if (v == u) ring_load<MTR>(R.a[v], N, N, u - rem);
-        }
+        for (int u = 0; u < RD; ++u)
+            if (u >= rem) ring_load<MTR>(R.a[u], N, N, u - rem);
     // slot u now holds step nfull + u + RD*(u < rem) of the A|N stream, i.e. N's step
-    // (u - rem) mod RD: rotate left by rem
+    // (u - rem) mod RD: rotate left by rem (rem is a compile-time constant wherever the
+    // shape is, and the selects fold away)
     f32x4 t[RD][MTR];
 #pragma unroll
     for (int u = 0; u < RD; ++u)
@@ -269,11 +265,11 @@ __device__ __forceinline__ void fz_gemm_impl(f32x4 (&acc)[MT][NF], int nf, ARing
     for (int u = 0; u < RD; ++u)
 #pragma unroll
         for (int i = 0; i < MTR; ++i) {
-            if constexpr (RD == 2) {
-                R.a[u][i] = t[(u + 1) & 1][i];   // rem == 1
-            } else {
-                R.a[u][i] = rem == 1 ? t[(u + 1) & 3][i] : (rem == 2 ? t[(u + 2) & 3][i] : t[(u + 3) & 3][i]);
-            }
+            f32x4 v = t[(u + 1) % RD][i];
+#pragma unroll
+            for (int r = 2; r < RD; ++r)
+                if (rem == r) v = t[(u + r) % RD][i];
+            R.a[u][i] = v;
         }
 }
 

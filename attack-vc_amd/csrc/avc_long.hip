@@ -25,6 +25,7 @@
 //
 // Per-layer frame counts are runtime values, but every GEMM runs a compile-time number of
 // fragments (8 per chunk; columns past the layer are clamped reads and dropped writes).
+#define AVC_FZ_RING_FREE 1   // no per-step scheduling barrier in the ring (fz_gemm_impl)
 #include "avc_fused_core.h"
 
 namespace avc {
