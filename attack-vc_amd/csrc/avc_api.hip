@@ -1315,7 +1315,10 @@ static bool want_fused(avc_ctx* ctx, int T) { return engine_for(ctx, T) != AVC_E
 
 // long-engine scratch for B utterances of up to T frames and `nlayers` masked layers
 static int alloc_long(LongArgs& L, int B, int T, int nlayers) {
-    const int rows = T + 2 * LZ_ZR + 64;
+    // a stride-2 chunk stages 2 * 127 + k + 2 input rows from row LZ_ZR - k/2 whatever the length,
+    // so a short utterance's image must still span them (T <= 178 read past the last image's end:
+    // an illegal address when that end was the end of a mapping)
+    const int rows = std::max(T, 2 * 128) + 2 * LZ_ZR + 64;
     L.img_stride = (int64_t)rows * 128 * 4;                 // fp32-sized rows serve both precisions
     L.fl_stride = (int64_t)((T + 32 + 15) / 16 + LZ_FL_EXTRA) * 4 * 2 * 64 * 4;
     L.nFmax = (T + 15) / 16;
@@ -1385,6 +1388,10 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     auto it = ctx->wss.begin();
     for (; it != ctx->wss.end(); ++it)
         if (it->built && it->B == B && it->T == T && it->fused == fused && it->lz == lz) break;
+    static const bool dbg_ws = getenv("AVC_DEBUG_WS") && getenv("AVC_DEBUG_WS")[0] == '1';
+    if (dbg_ws)
+        fprintf(stderr, "AVC_DEBUG_WS ensure_ws B=%d T=%d fused=%d lz=%d n=%d: %s (%zu cached)\n", B, T, (int)fused,
+                (int)lz, n_iters, it != ctx->wss.end() ? "hit" : "new", ctx->wss.size());
     if (it != ctx->wss.end()) {
         ctx->wss.splice(ctx->wss.begin(), ctx->wss, it);
         ctx->cur = &ctx->wss.front();
@@ -1398,6 +1405,9 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         const int cap = std::max(1, ce ? atoi(ce) : ctx->ws_cap);
         while ((int)ctx->wss.size() >= cap) {
             HIPCHK(hipStreamSynchronize(ctx->stream));
+            if (dbg_ws)
+                fprintf(stderr, "AVC_DEBUG_WS evict ws B=%d T=%d lz=%d gen=%d\n", ctx->wss.back().B, ctx->wss.back().T,
+                        (int)ctx->wss.back().lz, ctx->wss.back().gen);
             free_ws(ctx->wss.back());
             ctx->wss.pop_back();
             ++ctx->n_ws_evictions;
@@ -1723,9 +1733,19 @@ static int run_plan(avc_ctx* ctx, const Plan& pl, bool prof) {
     KEv ev;
     if (prof)
         for (hipEvent_t* e : {&ev.gemm0, &ev.gemm1, &ev.red0, &ev.red1}) HIPCHK(hipEventCreate(e));
+    static const bool dbg_sync = getenv("AVC_DEBUG_SYNC") && getenv("AVC_DEBUG_SYNC")[0] == '1';
     for (const Launch& L : pl.launches) {
         hipError_t e = launch_one(L, ctx->stream, prof ? &ev : nullptr);
         if (e != hipSuccess) return fail("launch %s: %s", kernel_name(L).c_str(), hipGetErrorString(e));
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (dbg_sync) (void)hipStreamIsCapturing(ctx->stream, &cs);
+        if (dbg_sync && cs == hipStreamCaptureStatusNone) {   // diagnostics: each launch completes before the next
+            e = hipStreamSynchronize(ctx->stream);
+            if (e != hipSuccess) {
+                fprintf(stderr, "AVC_DEBUG_SYNC: %s failed: %s\n", kernel_name(L).c_str(), hipGetErrorString(e));
+                return fail("kernel %s: %s", kernel_name(L).c_str(), hipGetErrorString(e));
+            }
+        }
         if (!prof) continue;
         const bool red = L.kind == L_GEMM && L.ksplit > 1;
         HIPCHK(hipEventSynchronize(red ? ev.red1 : ev.gemm1));

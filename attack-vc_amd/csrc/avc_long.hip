@@ -170,6 +170,47 @@ struct LzPipe {
     }
 };
 
+// x [80][T] frames u0 .. u0 + n - 1 -> LDS rows [0, n) (stride RS), transposed, frames outside
+// [0, T) by the bank's reflect pad (models.py:23-29; pads <= 4, rows further out are clamped
+// copies no owned column reads).  The fused engine's conflict-free mapping (lane (frame, half)
+// stores every other 16-byte channel group of its frame, avc_fused.hip), and all of a
+// thread's loads are issued before its first store: one HBM round trip.  n <= 256.
+template <int PREC>
+__device__ __forceinline__ void lz_x_window(char* XB, const float* xs, int T, int u0, int n) {
+    constexpr int RS = Lz<PREC>::RS, VE = 16 / Lz<PREC>::ESZ;
+    constexpr int NGX = FZ_CIN / VE, GPT = NGX / 2;
+    static_assert(NGX % 2 == 0, "channel groups split over two lanes");
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, xh = lane & 1;
+    float xv[2][GPT][VE];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int r = 128 * p + 32 * w + (lane >> 1);
+        int u = u0 + r;
+        u = u < 0 ? -u : (u >= T ? 2 * T - 2 - u : u);
+        u = min(max(u, 0), T - 1);
+        if (r < n)
+#pragma unroll
+            for (int m = 0; m < GPT; ++m)
+#pragma unroll
+                for (int e = 0; e < VE; ++e) xv[p][m][e] = xs[(size_t)((2 * m + xh) * VE + e) * T + u];
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int r = 128 * p + 32 * w + (lane >> 1);
+        if (r < n)
+#pragma unroll
+            for (int m = 0; m < GPT; ++m) {
+                f32x4 v;
+                if constexpr (PREC == PREC_F32) {
+                    v = f32x4{xv[p][m][0], xv[p][m][1], xv[p][m][2], xv[p][m][3]};
+                } else {
+                    v = pk_bf16x8([&](int e) { return xv[p][m][e]; });
+                }
+                *reinterpret_cast<f32x4*>(XB + r * RS + (2 * m + xh) * 16) = v;
+            }
+    }
+}
+
 // zero image rows [r0, r0 + n) (whole workgroup)
 template <int PREC>
 __device__ __forceinline__ void lz_zero_rows(char* img, int r0, int n) {
@@ -185,10 +226,14 @@ __device__ __forceinline__ void lz_publish() {
     __syncthreads();
 }
 
-// this lane's f32x4 of frame t (channels 32w + 16i + 4kq .. +3) in a fragment-layout stream
-__device__ __forceinline__ f32x4* lz_fl(float* buf, int t, int w, int i) {
+// this lane's f32x4 of frame t (channels 32w + 16i + 4kq .. +3) in a fragment-layout stream.
+// A global-address-space pointer: the streams are picked from pointer pairs (ping-pong), and a
+// generic pointer made every access a flat load / store, which waits on LDS traffic too
+// (vmcnt AND lgkmcnt) -- one full round trip per fragment in the epilogues
+typedef __attribute__((address_space(1))) f32x4 gf32x4;
+__device__ __forceinline__ gf32x4* lz_fl(float* buf, int t, int w, int i) {
     const int kq = (threadIdx.x & 63) >> 4;
-    return reinterpret_cast<f32x4*>(buf) + ((((t >> 4) * 4 + w) * 2 + i) * 64 + ((t & 15) | (kq << 4)));
+    return (gf32x4*)(buf) + ((((t >> 4) * 4 + w) * 2 + i) * 64 + ((t & 15) | (kq << 4)));
 }
 
 // frame t of an operand image, 4 consecutive channels at byte offset chb; mirror rows of
@@ -216,9 +261,13 @@ __device__ __forceinline__ void lz_mask_store(u64* words, const f32x4 (&y)[2]) {
 }
 struct LzMask {
     u64 b[8];
+    // the words of a (layer, fragment, wave) are wave-uniform and read-only in the kernels that
+    // read them (written by an earlier launch): scalar loads, which count in lgkmcnt and so never
+    // wait behind the epilogue's vector stores (a vector load after a store waits for the store)
     __device__ __forceinline__ void load(const u64* words) {
+        const __attribute__((address_space(4))) u64* p = (const __attribute__((address_space(4))) u64*)words;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) b[k] = words[k];
+        for (int k = 0; k < 8; ++k) b[k] = p[k];
     }
     __device__ __forceinline__ void none() {
 #pragma unroll
@@ -323,7 +372,6 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
     FZ_PH_DECL
     FZ_PH();
 
-    char* imgx = L.img[0] + (size_t)b * L.img_stride;
     char* imgh = L.img[1] + (size_t)b * L.img_stride;
     char* imgy = L.img[2] + (size_t)b * L.img_stride;
     float* hf[2] = {L.fl[0] + (size_t)b * L.fl_stride, L.fl[1] + (size_t)b * L.fl_stride};
@@ -349,26 +397,6 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
     ARing<2> ring;
     ring_fill(ring, op_bank(0));
 
-    // ---- x [80][T] -> image rows (transposed; reflect mirrors for the bank's pads <= 4)
-    {
-        constexpr int NGX = FZ_CIN / VE;
-        const float* xs = A.x + (size_t)b * FZ_CIN * T;
-        for (int idx = tid; idx < NGX * T; idx += 256) {
-            const int g = idx / T, t = idx - g * T;
-            f32x4 v;
-            if constexpr (PREC == PREC_F32) {
-                v = f32x4{xs[(size_t)(4 * g) * T + t], xs[(size_t)(4 * g + 1) * T + t], xs[(size_t)(4 * g + 2) * T + t],
-                          xs[(size_t)(4 * g + 3) * T + t]};
-            } else {
-                v = pk_bf16x8([&](int e) { return xs[(size_t)(8 * g + e) * T + t]; });
-            }
-            *reinterpret_cast<f32x4*>(imgx + (size_t)(LZ_ZR + t) * GRB + 16 * g) = v;
-            if (t >= 1 && t <= 4) *reinterpret_cast<f32x4*>(imgx + (size_t)(LZ_ZR - t) * GRB + 16 * g) = v;
-            if (t >= T - 5 && t <= T - 2)
-                *reinterpret_cast<f32x4*>(imgx + (size_t)(LZ_ZR + 2 * T - 2 - t) * GRB + 16 * g) = v;
-        }
-    }
-    lz_publish();
     FZ_PH();
 
     int rb[NF];
@@ -388,7 +416,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         for (int k = 0; lz_chunk(k, nf0, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
             __syncthreads();                             // the previous chunk's readers are done
-            lz_stage<PREC>(XB, imgx, LZ_ZR + n0 - 4, NXR);
+            lz_x_window<PREC>(XB, A.x + (size_t)b * FZ_CIN * T, T, n0 - 4, NXR);
             __syncthreads();
             FZ_PH();
             f32x4 acc_h[2][NF];
@@ -570,6 +598,25 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             const AOp nxt = chk.last ? (!lastblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l))) : op_c2(l);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l), nxt, SB, rb);
             FZ_PH();
+            // the residual inputs of the whole chunk are loaded before any of the epilogue's
+            // stores and before the next chunk's DMA: a load issued after a store waits for it
+            // (one vmcnt), so per fragment they cost a round trip each
+            f32x4 pa[NF][2], pb[NF][2];
+            if (!ce) {
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const int t = min(n0 + 16 * f + c, To - 1);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) pa[f][i] = *lz_fl(hin, s * t, w, i);
+                }
+                if (s == 2)
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) {
+                        const int t = min(n0 + 16 * f + c, To - 1);
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) pb[f][i] = *lz_fl(hin, min(2 * t + 1, Ti - 1), w, i);
+                    }
+            }
             pipe2.issue_next(k, imgy, r0_c2, nr_c2);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
@@ -590,7 +637,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                             *lz_fl(raw, t, w, i) = y[i];
                             if (chk.owns(t)) in_s[i] += y[i];
                         } else {
-                            const f32x4 h = y[i] + pool(t, i);
+                            // avg_pool1d(h, s, ceil_mode): (h[2t] + h[2t+1]) / 2, a lone tail frame as is
+                            const f32x4 pv = s == 1 ? pa[f][i] : (2 * t + 1 < Ti ? (pa[f][i] + pb[f][i]) / 2.f : pa[f][i]);
+                            const f32x4 h = y[i] + pv;
                             *lz_fl(hout, t, w, i) = h;
                             lz_put<PREC>(imgh, t, To, (ch0 + 16 * i) * ESZ, h);
                             if (lastblk && chk.owns(t)) tmean[i] += h;
@@ -823,6 +872,22 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                 fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), nxt, SB, rb);
             }
             FZ_PH();
+            // g(h_{l+1}) of the chunk's frames, loaded before the epilogue's stores (see the
+            // forward's conv2 epilogue)
+            f32x4 gq[NF][2];
+            if (l == nblk - 1) {
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) gq[f][i] = gN[i];
+            } else {
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const int t = min(max(16 * (chk.f0 + f - 1) + c, 0), Ti - 1);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) gq[f][i] = *lz_fl(gprev, s == 2 ? t >> 1 : t, w, i);
+                }
+            }
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
             pipeg2.issue_next(k, imgg2, r0_g, nr_g);
 #pragma unroll
@@ -838,10 +903,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                         f32x4 gp;
                         if (s == 2) {
                             const int tp = t >> 1;
-                            const f32x4 g = l == nblk - 1 ? gN[i] : *lz_fl(gprev, tp, w, i);
-                            gp = (2 * tp + 1 < Ti) ? g / 2.f : g;
+                            gp = (2 * tp + 1 < Ti) ? gq[f][i] / 2.f : gq[f][i];
                         } else {
-                            gp = l == nblk - 1 ? gN[i] : *lz_fl(gprev, t, w, i);
+                            gp = gq[f][i];
                         }
                         const f32x4 g = acc[i][f] + gp;
                         if (l > 0) *lz_fl(gnew, t, w, i) = g;
@@ -879,6 +943,10 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     static_assert(2 * FZ_CIN * CH * 4 <= 150 * 1024, "reduction rows overlap the fold scratch");
     float* R0 = reinterpret_cast<float*>(fz_lds);       // cross-wave partial sums (alias GP / GBK)
     float* R1 = R0 + FZ_CIN * CH;
+    // column of row ci rotated by 16 (ci / 4 mod 4): the 4 lane groups (kq) of a store then hit
+    // distinct banks instead of the same 16 (rows of CH floats all start on bank 0: a 4-way
+    // conflict).  (Padding the rows instead made the compiler spill the accumulators.)
+    auto rcol = [](int ci, int col) __attribute__((always_inline)) { return (col + 16 * ((ci >> 2) & 3)) & (CH - 1); };
     const int nfx = lz_nf(T + 8);
     const AdamArgs& Ad = A.adam;
     // gx_out mode (fb: d loss / d x handed on) has no Adam state: its AdamArgs are empty
@@ -977,7 +1045,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                     for (int f = 0; f < CHF; ++f)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            float* p = R + (16 * i + 4 * kq + r) * CH + 16 * f + c;
+                            float* p = R + (16 * i + 4 * kq + r) * CH + ((16 * f + c + 16 * kq) & (CH - 1));
                             *p = phase ? accx[i][f][r] + *p : accx[i][f][r];
                         }
             }
@@ -999,7 +1067,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                 const int n = n0 + col, t = n - 4;
                 ok[u] = idx < FZ_CIN * CH && chk.owns(n) && t >= 0 && t < T;
                 qv[u] = xb + (size_t)min(ci, FZ_CIN - 1) * T + min(max(t, 0), T - 1);
-                gs[u] = idx < FZ_CIN * CH ? R0[ci * CH + col] + R1[ci * CH + col] : 0.f;
+                gs[u] = idx < FZ_CIN * CH ? R0[ci * CH + rcol(ci, col)] + R1[ci * CH + rcol(ci, col)] : 0.f;
                 if (adam) {
                     P[u] = Ad.ptb[qv[u]];
                     M[u] = Ad.m[qv[u]];
