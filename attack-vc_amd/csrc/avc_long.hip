@@ -25,12 +25,25 @@
 //
 // Per-layer frame counts are runtime values, but every GEMM runs a compile-time number of
 // fragments (8 per chunk; columns past the layer are clamped reads and dropped writes).
+#ifndef LZ_RD
+#define LZ_RD 4              // weight-ring depth of the block / bank-forward GEMMs
+#endif
+#ifndef LZ_PIN
 #define AVC_FZ_RING_FREE 1   // no per-step scheduling barrier in the ring (fz_gemm_impl)
+#endif
 #include "avc_fused_core.h"
 
 namespace avc {
 
 constexpr int LZ_CHF = 8;           // fragments per chunk (128 columns)
+// finer stamps inside the bank phases (diagnostic builds with -DAVC_LZ_BANK_PHASES only)
+#ifdef AVC_LZ_BANK_PHASES
+#define FZ_PHB() FZ_PH()
+#else
+#define FZ_PHB() \
+    do {         \
+    } while (0)
+#endif
 
 template <int PREC>
 struct Lz {
@@ -220,6 +233,12 @@ __device__ __forceinline__ void lz_zero_rows(char* img, int r0, int n) {
     for (int i = threadIdx.x; i < tot; i += 256) p[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
+// wait for every vector-memory operation of this wave (s_waitcnt vmcnt(0), gfx9 encoding:
+// expcnt / lgkmcnt left at their maxima).  The builtin, unlike inline asm, is seen by the
+// compiler's waitcnt pass, so registers loaded before it need no further wait -- in particular
+// none behind the epilogue's branchy stores, where the pass can only wait for everything
+__device__ __forceinline__ void lz_vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // global stores of this workgroup visible to its other waves
 __device__ __forceinline__ void lz_publish() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -394,7 +413,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
     auto op_c1 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1[l], 2 * w, 2, ns_c, ns_c); };
     auto op_c2 = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2[l], 2 * w, 2, ns_c, ns_c); };
     auto op_mean = [&]() __attribute__((always_inline)) { return aop(A.w.mean_w, 2 * w, 2, FZ_C / KS, FZ_C / KS); };
-    ARing<2> ring;
+    ARing<2, LZ_RD> ring;
     ring_fill(ring, op_bank(0));
 
     FZ_PH();
@@ -432,6 +451,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
 #pragma unroll
                 for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T - 1) - n0 + 4 - pl;
                 fz_gemm<PREC, 2, NF, FZ_CIN, 1>(acc, IC<NF>{}, ring, op_bank(kb), op_inb(kb), XB, rb);
+                FZ_PHB();
                 char* BK = (kb & 1) ? BK1 : BK0;
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
@@ -448,8 +468,10 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
 #pragma unroll
                 for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T - 1) - n0;
                 const AOp nxt = kb + 1 < nb ? op_bank(kb + 1) : op_inx();
+                FZ_PHB();
                 fz_gemm<PREC, 2, NF, FZ_C, 1>(acc_h, IC<NF>{}, ring, op_inb(kb), nxt, BK, rb);
                 if (!DBUF) __syncthreads();
+                FZ_PHB();
             };
             for (int kb = 0; kb < nb; ++kb) bank_step(kb);
             FZ_PH();
@@ -598,24 +620,31 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             const AOp nxt = chk.last ? (!lastblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l))) : op_c2(l);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l), nxt, SB, rb);
             FZ_PH();
-            // the residual inputs of the whole chunk are loaded before any of the epilogue's
-            // stores and before the next chunk's DMA: a load issued after a store waits for it
-            // (one vmcnt), so per fragment they cost a round trip each
-            f32x4 pa[NF][2], pb[NF][2];
+            // the pooled residual of the whole chunk is loaded AND reduced before any of the
+            // epilogue's stores and before the next chunk's DMA: a load consumed after a store (or
+            // behind a branch that stores) waits for that store too (vmcnt counts both), which cost
+            // a round trip per fragment
+            f32x4 pv[NF][2];
             if (!ce) {
+                f32x4 pb[NF][2];
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
                     const int t = min(n0 + 16 * f + c, To - 1);
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) pa[f][i] = *lz_fl(hin, s * t, w, i);
-                }
-                if (s == 2)
-#pragma unroll
-                    for (int f = 0; f < NF; ++f) {
-                        const int t = min(n0 + 16 * f + c, To - 1);
-#pragma unroll
-                        for (int i = 0; i < 2; ++i) pb[f][i] = *lz_fl(hin, min(2 * t + 1, Ti - 1), w, i);
+                    for (int i = 0; i < 2; ++i) {
+                        pv[f][i] = *lz_fl(hin, s * t, w, i);
+                        pb[f][i] = *lz_fl(hin, min(2 * t + 1, Ti - 1), w, i);
                     }
+                }
+                lz_vm_drain();
+                // avg_pool1d(h, s, ceil_mode): (h[2t] + h[2t+1]) / 2, a lone tail frame as is
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const int t = n0 + 16 * f + c;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        if (s == 2 && 2 * t + 1 < Ti) pv[f][i] = (pv[f][i] + pb[f][i]) / 2.f;
+                }
             }
             pipe2.issue_next(k, imgy, r0_c2, nr_c2);
 #pragma unroll
@@ -637,9 +666,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                             *lz_fl(raw, t, w, i) = y[i];
                             if (chk.owns(t)) in_s[i] += y[i];
                         } else {
-                            // avg_pool1d(h, s, ceil_mode): (h[2t] + h[2t+1]) / 2, a lone tail frame as is
-                            const f32x4 pv = s == 1 ? pa[f][i] : (2 * t + 1 < Ti ? (pa[f][i] + pb[f][i]) / 2.f : pa[f][i]);
-                            const f32x4 h = y[i] + pv;
+                            const f32x4 h = y[i] + pv[f][i];
                             *lz_fl(hout, t, w, i) = h;
                             lz_put<PREC>(imgh, t, To, (ch0 + 16 * i) * ESZ, h);
                             if (lastblk && chk.owns(t)) tmean[i] += h;
@@ -752,7 +779,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     auto op_bankT = [&](int kb) __attribute__((always_inline)) {
         return aop(A.w.bankT[kb], 0, 5, (kb + 1) * SPT, (kb + 1) * SPW, LG, SPW - 1, SPT, w * SPW);
     };
-    ARing<2> ring;
+    ARing<2, LZ_RD> ring;
     ring_fill(ring, op_c2T(nblk - 1));
 
     // g(h_N) = d loss / d pooled / TN on every frame (AdaptiveAvgPool1d backward)
@@ -888,6 +915,15 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                     for (int i = 0; i < 2; ++i) gq[f][i] = *lz_fl(gprev, s == 2 ? t >> 1 : t, w, i);
                 }
             }
+            lz_vm_drain();
+            // torch avg_pool backward: grad / divide_factor (2, or 1 for a ceil tail)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = 16 * (chk.f0 + f - 1) + c;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    if (s == 2 && 2 * (t >> 1) + 1 < Ti) gq[f][i] = gq[f][i] / 2.f;
+            }
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
             pipeg2.issue_next(k, imgg2, r0_g, nr_g);
 #pragma unroll
@@ -899,15 +935,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                 if (t < Ti)
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
-                        // torch avg_pool backward: grad / divide_factor (2, or 1 for a ceil tail)
-                        f32x4 gp;
-                        if (s == 2) {
-                            const int tp = t >> 1;
-                            gp = (2 * tp + 1 < Ti) ? gq[f][i] / 2.f : gq[f][i];
-                        } else {
-                            gp = gq[f][i];
-                        }
-                        const f32x4 g = acc[i][f] + gp;
+                        const f32x4 g = acc[i][f] + gq[f][i];
                         if (l > 0) *lz_fl(gnew, t, w, i) = g;
                         f32x4 v;
 #pragma unroll
@@ -996,6 +1024,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
 #pragma unroll
             for (int f = 0; f < NFW; ++f) rt[f] = 16 * f + c;
             fz_gemm<PREC, 2, NFW, FZ_C, 1>(acc, IC<NFW>{}, ring5, op_inTb(kb), op_bankT(kb), GP, rt);
+            FZ_PHB();
 #pragma unroll
             for (int f = 0; f < NFW; ++f) {
                 const int F = W0 / 16 + f, u = 16 * F + c;
@@ -1013,6 +1042,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             // wave-local hand-off (as in se_bwd_fused): the bank^T below reads only this wave's
             // g(b_k) channels, and GP is read-only here -- program order, no workgroup barrier
             asm volatile("" ::: "memory");
+            FZ_PHB();
             // bank_k^T over this wave's channel quarter: rows u = v + pl - j of g(b_k)
 #pragma unroll
             for (int f = 0; f < LZ_CHF; ++f) {
@@ -1026,6 +1056,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                 fz_gemm<PREC, 5, LZ_CHF, FZ_C, -1>(accx, IC<CHF>{}, ring5, op_bankT(kb), nxt, GBK, rb);
             }
             asm volatile("" ::: "memory");   // (the next gate rewrites this wave's slice: in order)
+            FZ_PHB();
         };
         FZ_PH();
         for (int kb = 0; kb < nb; ++kb) bank_step(kb);
