@@ -36,6 +36,7 @@
 namespace avc {
 
 constexpr int LZ_CHF = 8;           // fragments per chunk (128 columns)
+constexpr int LZ_FB = 4;            // fragments per batch of the per-frame passes (loads, then stores)
 // finer stamps inside the bank phases (diagnostic builds with -DAVC_LZ_BANK_PHASES only)
 #ifdef AVC_LZ_BANK_PHASES
 #define FZ_PHB() FZ_PH()
@@ -265,35 +266,29 @@ __device__ __forceinline__ void lz_put(char* img, int t, int T, int chb, f32x4 v
     if (t >= T - 5 && t <= T - 2) st4<PREC>(img + (size_t)(LZ_ZR + 2 * T - 2 - t) * GRB + chb, v);
 }
 
-// ReLU' ballots of one fragment: word (i, r) bit (16 kq + c) = (y[i][r] > 0)
-__device__ __forceinline__ void lz_mask_store(u64* words, const f32x4 (&y)[2]) {
-    u64 b[8];
+// ReLU' bits of one fragment, one byte per lane: bit 4i + r = (y[i][r] > 0), the lane's own
+// elements.  Layout [layer][fragment][wave][lane] bytes per utterance (a wave's 64 bytes of a
+// fragment are one coalesced access).  VALU only (med3 of the float's bits, as MaskAcc): the former 64-bit ballots
+// parked one SGPR pair per element and stored through lane 0 under a branch, and were read back
+// per fragment with a scalar load whose lgkmcnt(0) wait also drained the LDS queue
+__device__ __forceinline__ unsigned lz_mask_bits(const f32x4 (&y)[2]) {
+    unsigned m = 0;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) b[4 * i + r] = __ballot(y[i][r] > 0.f);
-    if ((threadIdx.x & 63) == 0) {
-        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) reinterpret_cast<u64x2*>(words)[k] = u64x2{b[2 * k], b[2 * k + 1]};
-    }
+        for (int r = 0; r < 4; ++r) {
+            unsigned bit;
+            asm("v_med3_i32 %0, %1, 0, 1" : "=v"(bit) : "v"(y[i][r]));
+            m |= bit << (4 * i + r);
+        }
+    return m;
 }
 struct LzMask {
-    u64 b[8];
-    // the words of a (layer, fragment, wave) are wave-uniform and read-only in the kernels that
-    // read them (written by an earlier launch): scalar loads, which count in lgkmcnt and so never
-    // wait behind the epilogue's vector stores (a vector load after a store waits for the store)
-    __device__ __forceinline__ void load(const u64* words) {
-        const __attribute__((address_space(4))) u64* p = (const __attribute__((address_space(4))) u64*)words;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) b[k] = p[k];
-    }
-    __device__ __forceinline__ void none() {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) b[k] = 0;
-    }
+    unsigned bits;
+    __device__ __forceinline__ void load(const unsigned char* p) { bits = *p; }
+    __device__ __forceinline__ void none() { bits = 0; }
     __device__ __forceinline__ float act(int i, int r, int actk) const {
-        return ((b[4 * i + r] >> (threadIdx.x & 63)) & 1ull) ? 1.f : (actk ? 0.01f : 0.f);
+        return ((bits >> (4 * i + r)) & 1u) ? 1.f : (actk ? 0.01f : 0.f);
     }
 };
 
@@ -352,14 +347,24 @@ __device__ __forceinline__ void lz_in_stats(const float* raw, int Tl, int w, f32
     }
     f32x4 q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int nf = lz_nf(Tl);
-    for (int F = 0; F < nf; ++F) {
-        const int t = 16 * F + c;
-        if (t < Tl)
+    // LZ_FB fragments' loads in flight at a time (a runtime loop of load -> use waited a round
+    // trip per fragment); the sum runs in the same fragment order
+    for (int F0 = 0; F0 < nf; F0 += LZ_FB) {
+        f32x4 v[LZ_FB][2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const f32x4 d = *lz_fl(const_cast<float*>(raw), t, w, i) - mean[i];
-                q[i] += d * d;
-            }
+        for (int u = 0; u < LZ_FB; ++u)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) v[u][i] = *lz_fl(const_cast<float*>(raw), min(16 * (F0 + u) + c, Tl - 1), w, i);
+#pragma unroll
+        for (int u = 0; u < LZ_FB; ++u) {
+            const int t = 16 * (F0 + u) + c;
+            if (t < Tl)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const f32x4 d = v[u][i] - mean[i];
+                    q[i] += d * d;
+                }
+        }
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -395,9 +400,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
     char* imgy = L.img[2] + (size_t)b * L.img_stride;
     float* hf[2] = {L.fl[0] + (size_t)b * L.fl_stride, L.fl[1] + (size_t)b * L.fl_stride};
     float* raw = L.fl[2] + (size_t)b * L.fl_stride;
-    u64* mk = L.masks + (size_t)b * L.mask_stride;
-    auto mword = [&](int layer, int F) __attribute__((always_inline)) {
-        return mk + ((size_t)(layer * L.nFmax + F) * 4 + w) * 8;
+    unsigned char* mk = reinterpret_cast<unsigned char*>(L.masks + (size_t)b * L.mask_stride);
+    auto mbyte = [&](int layer, int F) __attribute__((always_inline)) {
+        return mk + ((size_t)(layer * L.nFmax + F) * 4 + w) * 64 + lane;
     };
 
     const int ns_c = ks * FZ_C / KS;
@@ -460,7 +465,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
                     for (int i = 0; i < 2; ++i)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) y[i][r] = act_f(acc[i][f][r] + bkb[i][r], act);
-                    if (wm && chk.f0 + f < nf0 && chk.owns(16 * (chk.f0 + f))) lz_mask_store(mword(kb, chk.f0 + f), y);
+                    if (wm && chk.f0 + f < nf0 && chk.owns(16 * (chk.f0 + f))) *mbyte(kb, chk.f0 + f) = (unsigned char)lz_mask_bits(y);
 #pragma unroll
                     for (int i = 0; i < 2; ++i) st4<PREC>(BK + (16 * f + c) * RS + (ch0 + 16 * i) * ESZ, y[i]);
                 }
@@ -491,7 +496,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) y[i][r] = act_f(y[i][r], act);
                 }
-                if (wm && chk.f0 + f < nf0 && chk.owns(16 * (chk.f0 + f))) lz_mask_store(mword(nb, chk.f0 + f), y);
+                if (wm && chk.f0 + f < nf0 && chk.owns(16 * (chk.f0 + f))) *mbyte(nb, chk.f0 + f) = (unsigned char)lz_mask_bits(y);
                 if (t < T)
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
@@ -575,7 +580,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) y[i][r] = act_f(y[i][r], act);
                 }
-                if (wm && chk.f0 + f < nfi && chk.owns(16 * (chk.f0 + f))) lz_mask_store(mword(nb + 1 + 2 * l, chk.f0 + f), y);
+                if (wm && chk.f0 + f < nfi && chk.owns(16 * (chk.f0 + f))) *mbyte(nb + 1 + 2 * l, chk.f0 + f) = (unsigned char)lz_mask_bits(y);
                 if (t < Ti)
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
@@ -658,7 +663,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) y[i][r] = act_f(y[i][r], act);
                 }
-                if (wm && chk.f0 + f < nfo && chk.owns(16 * (chk.f0 + f))) lz_mask_store(mword(nb + 2 + 2 * l, chk.f0 + f), y);
+                if (wm && chk.f0 + f < nfo && chk.owns(16 * (chk.f0 + f))) *mbyte(nb + 2 + 2 * l, chk.f0 + f) = (unsigned char)lz_mask_bits(y);
                 if (t < To)
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
@@ -760,9 +765,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     char* imgg = L.img[1] + (size_t)b * L.img_stride;   // dilated dY of a conv2
     char* imgg2 = L.img[2] + (size_t)b * L.img_stride;  // dY of a conv1
     float* gh[2] = {L.fl[0] + (size_t)b * L.fl_stride, L.fl[1] + (size_t)b * L.fl_stride};
-    const u64* mk = L.masks + (size_t)b * L.mask_stride;
-    auto mword = [&](int layer, int F) __attribute__((always_inline)) {
-        return mk + ((size_t)(layer * L.nFmax + F) * 4 + w) * 8;
+    const unsigned char* mk = reinterpret_cast<const unsigned char*>(L.masks + (size_t)b * L.mask_stride);
+    auto mbyte = [&](int layer, int F) __attribute__((always_inline)) {
+        return mk + ((size_t)(layer * L.nFmax + F) * 4 + w) * 64 + lane;
     };
     float* FSCR = reinterpret_cast<float*>(fz_lds + 150 * 1024) + w * (5 * 16 * 8);
     FZ_PH_DECL
@@ -796,7 +801,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         const int l = nblk - 1, To = A.Tl[l + 1], s = A.sub[l];
         for (int F = 0; F < lz_nf(To); ++F) {
             LzMask m;
-            m.load(mword(nb + 2 + 2 * l, F));
+            m.load(mbyte(nb + 2 + 2 * l, F));
             const int t = 16 * F + c;
             if (t < To)
 #pragma unroll
@@ -847,14 +852,17 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c2T(l), chk.last ? op_c1T(l) : op_c2T(l), SB, rb);
             FZ_PH();
+            LzMask mv[NF];   // the chunk's ReLU' bytes, loaded before the epilogue's stores
+#pragma unroll
+            for (int f = 0; f < NF; ++f) mv[f].load(mbyte(nb + 1 + 2 * l, min(max(chk.f0 + f - 1, 0), lz_nf(Ti) - 1)));
+            lz_vm_drain();
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
             pipeg.issue_next(k, imgg, r0_g, nr_g);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int F = chk.f0 + f - 1, t = 16 * F + c;   // frame of the column
                 if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
-                LzMask m;
-                m.load(mword(nb + 1 + 2 * l, F));
+                const LzMask m = mv[f];
                 if (t < Ti)
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
@@ -915,6 +923,9 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
                     for (int i = 0; i < 2; ++i) gq[f][i] = *lz_fl(gprev, s == 2 ? t >> 1 : t, w, i);
                 }
             }
+            LzMask mv[NF];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) mv[f].load(mbyte(mlayer, min(max(chk.f0 + f - 1, 0), lz_nf(Ti) - 1)));
             lz_vm_drain();
             // torch avg_pool backward: grad / divide_factor (2, or 1 for a ceil tail)
 #pragma unroll
@@ -930,8 +941,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             for (int f = 0; f < NF; ++f) {
                 const int F = chk.f0 + f - 1, t = 16 * F + c;
                 if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
-                LzMask m;
-                m.load(mword(mlayer, F));
+                const LzMask m = mv[f];
                 if (t < Ti)
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
@@ -1023,14 +1033,16 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
             int rt[NFW];
 #pragma unroll
             for (int f = 0; f < NFW; ++f) rt[f] = 16 * f + c;
+            LzMask mv[NFW];   // loaded ahead of the GEMM (they land under it)
+#pragma unroll
+            for (int f = 0; f < NFW; ++f) mv[f].load(mbyte(kb, min(max(W0 / 16 + f, 0), lz_nf(T) - 1)));
             fz_gemm<PREC, 2, NFW, FZ_C, 1>(acc, IC<NFW>{}, ring5, op_inTb(kb), op_bankT(kb), GP, rt);
             FZ_PHB();
 #pragma unroll
             for (int f = 0; f < NFW; ++f) {
                 const int F = W0 / 16 + f, u = 16 * F + c;
-                LzMask m;
-                if (F >= 0 && 16 * F < T) m.load(mword(kb, F));
-                else m.none();
+                LzMask m = mv[f];
+                if (!(F >= 0 && 16 * F < T)) m.none();
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     f32x4 v;
@@ -1148,16 +1160,31 @@ template <int PREC, int C>
 __device__ __forceinline__ void lz_ct_to_img(char* img, const float* src, int T) {
     using Z = Lz<PREC>;
     constexpr int VE = 16 / Z::ESZ, NG = C / VE;
-    for (int idx = threadIdx.x; idx < NG * T; idx += 256) {
-        const int g = idx / T, t = idx - g * T;
-        f32x4 v;
-        if constexpr (PREC == PREC_F32) {
-            v = f32x4{src[(size_t)(4 * g) * T + t], src[(size_t)(4 * g + 1) * T + t], src[(size_t)(4 * g + 2) * T + t],
-                      src[(size_t)(4 * g + 3) * T + t]};
-        } else {
-            v = pk_bf16x8([&](int e) { return src[(size_t)(8 * g + e) * T + t]; });
+    constexpr int U = 4;   // slots per thread in flight: their loads, one drain, then the stores
+    const int n = NG * T;
+    for (int base = threadIdx.x; base < n; base += 256 * U) {
+        float x[U][VE];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int idx = min(base + 256 * u, n - 1);
+            const int g = idx / T, t = idx - g * T;
+#pragma unroll
+            for (int e = 0; e < VE; ++e) x[u][e] = src[(size_t)(VE * g + e) * T + t];
         }
-        *reinterpret_cast<f32x4*>(img + (size_t)(LZ_ZR + t) * Z::GRB + 16 * g) = v;
+        lz_vm_drain();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int idx = base + 256 * u;
+            if (idx >= n) continue;
+            const int g = idx / T, t = idx - g * T;
+            f32x4 v;
+            if constexpr (PREC == PREC_F32) {
+                v = f32x4{x[u][0], x[u][1], x[u][2], x[u][3]};
+            } else {
+                v = pk_bf16x8([&](int e) { return x[u][e]; });
+            }
+            *reinterpret_cast<f32x4*>(img + (size_t)(LZ_ZR + t) * Z::GRB + 16 * g) = v;
+        }
     }
 }
 
@@ -1227,24 +1254,41 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
             }
         }
     }
-    // InstanceNorm over the Tl frames of raw, then out(t, i, yhat, invstd)
-    auto in_pass = [&](int Tl, auto&& out) __attribute__((always_inline)) {
+    // InstanceNorm over the Tl frames of raw, then out(t, i, yhat, invstd, ex) with ex = ld(t, i)
+    // (the residual, or nothing).  LZ_FB fragments at a time: all their loads, one drain, then the
+    // stores (a load consumed behind a store waits for the store: a round trip per fragment)
+    auto in_pass = [&](int Tl, auto&& ld, auto&& out) __attribute__((always_inline)) {
         lz_publish();
         f32x4 mean[2], inv[2];
         lz_in_stats(raw, Tl, w, in_s, mean, inv);
-        for (int F = 0; F < lz_nf(Tl); ++F) {
-            const int t = 16 * F + c;
-            if (t < Tl)
+        for (int F0 = 0; F0 < lz_nf(Tl); F0 += LZ_FB) {
+            f32x4 v[LZ_FB][2], ex[LZ_FB][2];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) out(t, i, (*lz_fl(raw, t, w, i) - mean[i]) * inv[i], inv[i]);
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int tc = min(16 * (F0 + u) + c, Tl - 1);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    v[u][i] = *lz_fl(raw, tc, w, i);
+                    ex[u][i] = ld(tc, i);
+                }
+            }
+            lz_vm_drain();
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int t = 16 * (F0 + u) + c;
+                if (t < Tl)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) out(t, i, (v[u][i] - mean[i]) * inv[i], inv[i], ex[u][i]);
+            }
         }
         in_s[0] = in_s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
+    auto no_ld = [](int, int) __attribute__((always_inline)) { return f32x4{0.f, 0.f, 0.f, 0.f}; };
     auto put_inv = [&](int q, const f32x4& inv, int i) __attribute__((always_inline)) {
         if (stash && c == 0)
             *reinterpret_cast<f32x4*>(A.invstd + ((size_t)b * 2 * nblk + q) * 128 + ch0 + 16 * i) = inv;
     };
-    in_pass(T0, [&](int t, int i, f32x4 v, f32x4) __attribute__((always_inline)) {
+    in_pass(T0, no_ld, [&](int t, int i, f32x4 v, f32x4, f32x4) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = act_f(v[r], act);
         *lz_fl(hf[0], t, w, i) = v;
@@ -1292,7 +1336,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
             }
         }
         float* st1 = stb + A.stash_off[2 * l];
-        in_pass(Ti, [&](int t, int i, f32x4 yh, f32x4 inv) __attribute__((always_inline)) {
+        in_pass(Ti, no_ld, [&](int t, int i, f32x4 yh, f32x4 inv, f32x4) __attribute__((always_inline)) {
             if (stash) *lz_fl(st1, t, w, i) = yh;
             if (t == c) put_inv(2 * l, inv, i);
             f32x4 v;
@@ -1332,13 +1376,14 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         float* hin = hf[cur];
         float* hout = hf[cur ^ 1];
         // IN over the To frames -> AdaIN(2l+1) -> act -> + (nearest-upsampled) residual
-        in_pass(To, [&](int t, int i, f32x4 yh, f32x4 inv) __attribute__((always_inline)) {
+        in_pass(To, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(hin, up == 2 ? t >> 1 : t, w, i)); },
+                [&](int t, int i, f32x4 yh, f32x4 inv, f32x4 res) __attribute__((always_inline)) {
             if (stash) *lz_fl(st2, t, w, i) = yh;
             if (t == c) put_inv(2 * l + 1, inv, i);
             f32x4 v;
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = act_f(yh[r] * sd2[i][r] + mn2[i][r], act);
-            const f32x4 h = v + *lz_fl(hin, up == 2 ? t >> 1 : t, w, i);
+            const f32x4 h = v + res;
             *lz_fl(hout, t, w, i) = h;
             lz_put<PREC>(imgh, t, To, (ch0 + 16 * i) * ESZ, h);
         });
@@ -1378,19 +1423,39 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         }
         __syncthreads();
         float* outb = A.out + (size_t)b * DZ_COUT * Tn;
-        for (int idx = tid; idx < DZ_COUT * 128; idx += 256) {
-            const int co = idx >> 7, col = idx & 127;
-            const int t = n0 + col;
-            if (t >= Tn || !chk.owns(t)) continue;
-            const float o = OS[idx];
-            const size_t q = (size_t)co * Tn + t;
-            outb[q] = o;
+        // UO elements per thread at a time: the targets' loads, one drain, then the stores (the
+        // same per-thread order of the loss sums)
+        constexpr int UO = 10;
+        for (int i0 = tid; i0 < DZ_COUT * 128; i0 += 256 * UO) {
+            float tg[UO], og[UO];
             if (e2e) {
-                const size_t qb = (size_t)b * DZ_COUT * Tn + q;
-                const float d1 = o - A.tgt_out[qb], d2 = o - A.org_out[qb];
-                A.g_out[qb] = gscale * d1 + gscale * d2 * -0.1f;
-                q1 += d1 * d1;
-                q2 += d2 * d2;
+#pragma unroll
+                for (int u = 0; u < UO; ++u) {
+                    const int idx = min(i0 + 256 * u, DZ_COUT * 128 - 1);
+                    const int co = idx >> 7, t = min(n0 + (idx & 127), Tn - 1);
+                    const size_t qb = (size_t)b * DZ_COUT * Tn + (size_t)co * Tn + t;
+                    tg[u] = A.tgt_out[qb];
+                    og[u] = A.org_out[qb];
+                }
+                lz_vm_drain();
+            }
+#pragma unroll
+            for (int u = 0; u < UO; ++u) {
+                const int idx = i0 + 256 * u;
+                if (idx >= DZ_COUT * 128) continue;
+                const int co = idx >> 7, col = idx & 127;
+                const int t = n0 + col;
+                if (t >= Tn || !chk.owns(t)) continue;
+                const float o = OS[idx];
+                const size_t q = (size_t)co * Tn + t;
+                outb[q] = o;
+                if (e2e) {
+                    const size_t qb = (size_t)b * DZ_COUT * Tn + q;
+                    const float d1 = o - tg[u], d2 = o - og[u];
+                    A.g_out[qb] = gscale * d1 + gscale * d2 * -0.1f;
+                    q1 += d1 * d1;
+                    q2 += d2 * d2;
+                }
             }
         }
     }
@@ -1495,20 +1560,34 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
             gm[i] = gs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
         lz_publish();
-        for (int F = 0; F < lz_nf(Tl); ++F) {
-            const int t = 16 * F + c;
-            if (t < Tl)
+        // LZ_FB fragments at a time: loads, one drain, then arithmetic and stores (in_pass)
+        for (int F0 = 0; F0 < lz_nf(Tl); F0 += LZ_FB) {
+            f32x4 gv[LZ_FB][2], yv[LZ_FB][2];
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int tc = min(16 * (F0 + u) + c, Tl - 1);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const f32x4 g = gsrc(t, i);
-                    const f32x4 yh = *lz_fl(const_cast<float*>(yq), t, w, i);
-                    f32x4 z;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) z[r] = g[r] * act_d(yh[r] * sd[i][r] + mn[i][r], act);
-                    *lz_fl(tmp, t, w, i) = z;
-                    gm[i] += z;
-                    gs[i] += z * yh;
+                    gv[u][i] = gsrc(tc, i);
+                    yv[u][i] = *lz_fl(const_cast<float*>(yq), tc, w, i);
                 }
+            }
+            lz_vm_drain();
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int t = 16 * (F0 + u) + c;
+                if (t < Tl)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const f32x4 g = gv[u][i], yh = yv[u][i];
+                        f32x4 z;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) z[r] = g[r] * act_d(yh[r] * sd[i][r] + mn[i][r], act);
+                        *lz_fl(tmp, t, w, i) = z;
+                        gm[i] += z;
+                        gs[i] += z * yh;
+                    }
+            }
         }
         f32x4 k1[2], k2[2], k3[2];
         const float inv_n = 1.f / (float)Tl;
@@ -1528,18 +1607,31 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
             }
         }
         lz_publish();
-        for (int F = 0; F < lz_nf(Tl); ++F) {
-            const int t = 16 * F + c;
-            if (t < Tl)
+        for (int F0 = 0; F0 < lz_nf(Tl); F0 += LZ_FB) {
+            f32x4 zv[LZ_FB][2], yv[LZ_FB][2];
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int tc = min(16 * (F0 + u) + c, Tl - 1);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const f32x4 z = *lz_fl(tmp, t, w, i);
-                    const f32x4 yh = *lz_fl(const_cast<float*>(yq), t, w, i);
-                    f32x4 d;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) d[r] = k1[i][r] * (z[r] - k2[i][r] - yh[r] * k3[i][r]);
-                    out(t, i, d);
+                    zv[u][i] = *lz_fl(tmp, tc, w, i);
+                    yv[u][i] = *lz_fl(const_cast<float*>(yq), tc, w, i);
                 }
+            }
+            lz_vm_drain();
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int t = 16 * (F0 + u) + c;
+                if (t < Tl)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const f32x4 z = zv[u][i], yh = yv[u][i];
+                        f32x4 d;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) d[r] = k1[i][r] * (z[r] - k2[i][r] - yh[r] * k3[i][r]);
+                        out(t, i, d);
+                    }
+            }
         }
     };
 
@@ -1550,7 +1642,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
         float* gout = gh[cur ^ 1];       // g(h_l) over Ti frames
         // conv2 branch: act, AdaIN(2l+1), IN backward over To frames -> dY image(s): frame
         // 2t + s of the shuffled output is half s of frame t
-        adain_in_bwd(2 * l + 1, To, [&](int t, int i) __attribute__((always_inline)) { return *lz_fl(gin, t, w, i); },
+        adain_in_bwd(2 * l + 1, To, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(gin, t, w, i)); },
                      [&](int t, int i, f32x4 d) __attribute__((always_inline)) {
                          char* im = (up == 2 && (t & 1)) ? imgg2 : imgg;
                          const int tt = up == 2 ? t >> 1 : t;
@@ -1597,11 +1689,11 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
         // conv1 branch: act, AdaIN(2l), IN backward -> dY of conv1 (the first block stops: mu
         // is constant in the attacks)
         if (l == 0) {
-            adain_in_bwd(0, Ti, [&](int t, int i) __attribute__((always_inline)) { return *lz_fl(gout, t, w, i); },
+            adain_in_bwd(0, Ti, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(gout, t, w, i)); },
                          [&](int, int, f32x4) __attribute__((always_inline)) {});
             break;
         }
-        adain_in_bwd(2 * l, Ti, [&](int t, int i) __attribute__((always_inline)) { return *lz_fl(gout, t, w, i); },
+        adain_in_bwd(2 * l, Ti, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(gout, t, w, i)); },
                      [&](int t, int i, f32x4 d) __attribute__((always_inline)) {
                          st4<PREC>(imgg + (size_t)(LZ_ZR + t) * GRB + (ch0 + 16 * i) * ESZ, d);
                      });
@@ -1625,6 +1717,29 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), chk.last ? op_c2T(l - 1, 0) : op_c1T(l),
                                            WB, rb);
+            // the residual branch's gradient of the chunk, loaded and summed before the stores
+            f32x4 res[NF][2];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = min(max(16 * (chk.f0 + f - 1) + c, 0), Ti - 1);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) res[f][i] = *lz_fl(gin, up * t, w, i);
+            }
+            if (up == 2) {
+                f32x4 r1[NF][2];
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const int t = min(max(16 * (chk.f0 + f - 1) + c, 0), Ti - 1);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) r1[f][i] = *lz_fl(gin, 2 * t + 1, w, i);
+                }
+                lz_vm_drain();
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) res[f][i] = res[f][i] + r1[f][i];
+            }
+            lz_vm_drain();
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
@@ -1632,11 +1747,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
                 if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
                 if (t < Ti)
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const f32x4 res = up == 2 ? *lz_fl(gin, 2 * t, w, i) + *lz_fl(gin, 2 * t + 1, w, i)
-                                                  : *lz_fl(gin, t, w, i);
-                        *lz_fl(gout, t, w, i) = res + acc[i][f];
-                    }
+                    for (int i = 0; i < 2; ++i) *lz_fl(gout, t, w, i) = res[f][i] + acc[i][f];
             }
         }
         cur ^= 1;

@@ -558,6 +558,10 @@ def main():
                 roof["mfma_util"] = rec["mfma_util"]
                 roof["pmc_source"] = rec["source"]
                 roof["pmc_median_us"] = rec["median_us"]
+                # counters of another build than the one measured here are flagged, not passed off
+                ver = avc_native.lib().avc_version().decode()
+                roof["pmc_src"] = rec.get("src")
+                roof["pmc_stale"] = rec.get("src") is None or ("src=" + rec["src"]) not in ver
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -71,6 +71,18 @@ def load_trace(d, warm):
     return dur
 
 
+def src_hash(d):
+    """libavc source hash of the profiled binary (avc_bench logs avc_version() to stderr; the
+    trace pass's log sits next to the profile directory as <dir>.trace.log)."""
+    import re
+    for f in (d.rstrip("/") + ".trace.log",):
+        if os.path.exists(f):
+            m = re.search(r"libavc [^;\n]*src=([0-9a-f]{16})", open(f).read())
+            if m:
+                return m.group(1)
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -80,6 +92,7 @@ def main():
                                                       "under --key (read by bench.py)")
     ap.add_argument("--key", default=None, help="e.g. emb, emb_fp32, e2e, fb")
     a = ap.parse_args()
+    src = src_hash(a.dir)
     per = load_counters(a.dir, a.warm)
     dur = load_trace(a.dir, a.warm)
     rows = []
@@ -120,7 +133,7 @@ def main():
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out + "_summary.md", "w") as fh:
-            fh.write(f"# {os.path.basename(a.out)}\n\nSource: `{a.dir}` (rocprofv3 kernel trace + PMC passes of "
+            fh.write(f"# {os.path.basename(a.out)}\n\nlibavc src={src}.  Source: `{a.dir}` (rocprofv3 kernel trace + PMC passes of "
                      f"avc_bench; first {a.warm} dispatches per kernel skipped).  MFMA util = "
                      "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8).  HBM = 2 x FETCH_SIZE + "
                      "WRITE_SIZE.  Wave state = fractions of SQ_WAVE_CYCLES.\n\n" + txt + "\n")
@@ -131,7 +144,7 @@ def main():
     if a.pmc_json and a.key:
         db = json.load(open(a.pmc_json)) if os.path.exists(a.pmc_json) else {}
         db[a.key] = {libname(k): {"traffic": d["hbm_bytes"], "mfma_util": d["mfma_util"], "median_us": d["median_us"],
-                                  "source": (a.out or a.dir) + "_summary.md"} for k, d in rows}
+                                  "source": (a.out or a.dir) + "_summary.md", "src": src} for k, d in rows}
         json.dump(db, open(a.pmc_json, "w"), indent=1, sort_keys=True)
 
 
