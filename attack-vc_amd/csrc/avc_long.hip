@@ -1313,16 +1313,20 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         // conv1 -> raw -> IN -> AdaIN(2l) -> act -> imgy
         LzChunk chk;
         const int nfi = lz_nf(Ti);
+        // chunk windows staged by LDS-DMA one chunk ahead (LzPipe, as the SpeakerEncoder blocks)
+        auto r0_w = [=](const LzChunk& ch) __attribute__((always_inline)) { return LZ_ZR + 16 * ch.f0 - P; };
+        auto nr_w = [=](const LzChunk&) __attribute__((always_inline)) { return 127 + ks + 2; };
+        LzPipe<PREC, 136> pipe1(WB, nfi, 127 + ks + 2);
+        pipe1.prime(imgh, r0_w, nr_w);
         for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
-            __syncthreads();
-            lz_stage<PREC>(WB, imgh, LZ_ZR + n0 - P, 127 + ks + 2);
-            __syncthreads();
+            const char* SB = pipe1.next(k, chk, imgh, r0_w, nr_w);
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Ti - 1) - n0;
             f32x4 acc[2][NF];
             zero_acc(acc);
-            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c1(l), chk.last ? op_c2(l, 0) : op_c1(l), WB, rb);
+            fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c1(l), chk.last ? op_c2(l, 0) : op_c1(l), SB, rb);
+            pipe1.issue_next(k, imgh, r0_w, nr_w);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int t = n0 + 16 * f + c;
@@ -1347,18 +1351,19 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         lz_publish();
         // conv2 (up = 1: one GEMM; up = 2: the even / odd half-GEMMs) -> raw over To frames
         const AOp nxt = l + 1 < nblk ? op_c1(l + 1) : op_out();
+        LzPipe<PREC, 136> pipe2(WB, nfi, 127 + ks + 2);
+        pipe2.prime(imgy, r0_w, nr_w);
         for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
-            __syncthreads();
-            lz_stage<PREC>(WB, imgy, LZ_ZR + n0 - P, 127 + ks + 2);
-            __syncthreads();
+            const char* SB = pipe2.next(k, chk, imgy, r0_w, nr_w);
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Ti - 1) - n0;
             for (int s = 0; s < up; ++s) {
                 f32x4 acc[2][NF];
                 zero_acc(acc);
                 const AOp nx = s + 1 < up ? op_c2(l, 1) : (chk.last ? nxt : op_c2(l, 0));
-                fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l, s), nx, WB, rb);
+                fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l, s), nx, SB, rb);
+                if (s + 1 == up) pipe2.issue_next(k, imgy, r0_w, nr_w);
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
                     const int t = n0 + 16 * f + c;
@@ -1701,13 +1706,18 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
         lz_zero_rows<PREC>(imgg, LZ_ZR + Ti, LZ_ZR);
         lz_publish();
         // conv1^T (+ fold) + the residual branch (adjoint of the x2 nearest upsample) -> g(h_l)
+        auto r0_g = [=](const LzChunk& ch) __attribute__((always_inline)) {
+            return LZ_ZR + max(16 * ch.f0 - 16, -P) + P - ks - 1;
+        };
+        auto nr_g = [=](const LzChunk& ch) __attribute__((always_inline)) {
+            return min(16 * ch.f0 + 111, Ti + P - 1) - max(16 * ch.f0 - 16, -P) + ks + 2;
+        };
+        LzPipe<PREC, 136> pipeg(WB, nfc, 127 + ks + 2);
+        pipeg.prime(imgg, r0_g, nr_g);
         for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
-            const int vlo = max(n0 - 16, -P), vhi = min(n0 + 111, Ti + P - 1);
-            const int r0 = LZ_ZR + vlo + P - ks - 1;
-            __syncthreads();
-            lz_stage<PREC>(WB, imgg, r0, vhi - vlo + ks + 2);
-            __syncthreads();
+            const int r0 = r0_g(chk);
+            const char* SB = pipeg.next(k, chk, imgg, r0_g, nr_g);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 const int v = min(max(n0 + 16 * f + c - 16, -P), Ti + P - 1);
@@ -1716,7 +1726,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
             f32x4 acc[2][NF];
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c1T(l), chk.last ? op_c2T(l - 1, 0) : op_c1T(l),
-                                           WB, rb);
+                                           SB, rb);
             // the residual branch's gradient of the chunk, loaded and summed before the stores
             f32x4 res[NF][2];
 #pragma unroll
@@ -1740,6 +1750,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
                     for (int i = 0; i < 2; ++i) res[f][i] = res[f][i] + r1[f][i];
             }
             lz_vm_drain();
+            pipeg.issue_next(k, imgg, r0_g, nr_g);   // after the drain: it would wait for the DMA too
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {

@@ -9,7 +9,7 @@ for line in open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/phl.log"):
     if len(p) == 4 and p[0] in ("lfwd", "lbwd") and p[1].startswith("w"):
         seq[(p[0], p[1])].append((int(p[2]), int(p[3])))
 for tag in ("lfwd", "lbwd"):
-    for w in ("w0",):
+    for w in ("w0", "w1", "w2", "w3"):
         runs = []
         for i, v in seq[(tag, w)]:
             if i == 1:
