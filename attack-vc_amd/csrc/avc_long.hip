@@ -256,6 +256,31 @@ __device__ __forceinline__ gf32x4* lz_fl(float* buf, int t, int w, int i) {
     return (gf32x4*)(buf) + ((((t >> 4) * 4 + w) * 2 + i) * 64 + ((t & 15) | (kq << 4)));
 }
 
+// The Decoder's stash of normalised activations (written by the forward, read twice by the
+// backward: its dominant HBM stream at long T) in the fragment layout of lz_fl: fp32, or in bf16
+// mode packed bf16 (8 bytes per lane and fragment) -- the values the fused engine stashes too
+template <int PREC>
+__device__ __forceinline__ void lz_stash_put(float* buf, int t, int w, int i, const f32x4& v) {
+    if constexpr (PREC == PREC_F32) {
+        *lz_fl(buf, t, w, i) = v;
+    } else {
+        const size_t k = (size_t)(lz_fl(buf, t, w, i) - (gf32x4*)buf);
+        ((__attribute__((address_space(1))) u32x2*)buf)[k] = pk_bf16x4(v);
+    }
+}
+template <int PREC>
+__device__ __forceinline__ f32x4 lz_stash_get(const float* buf, int t, int w, int i) {
+    if constexpr (PREC == PREC_F32) {
+        return *lz_fl(const_cast<float*>(buf), t, w, i);
+    } else {
+        const size_t k = (size_t)(lz_fl(const_cast<float*>(buf), t, w, i) - (gf32x4*)buf);
+        const u32x2 v = ((const __attribute__((address_space(1))) u32x2*)buf)[k];
+        // bf16 -> f32 is exact: the bf16 bits in the high half
+        return f32x4{__builtin_bit_cast(float, v[0] << 16), __builtin_bit_cast(float, v[0] & 0xffff0000u),
+                     __builtin_bit_cast(float, v[1] << 16), __builtin_bit_cast(float, v[1] & 0xffff0000u)};
+    }
+}
+
 // frame t of an operand image, 4 consecutive channels at byte offset chb; mirror rows of
 // the reflect pad (F.pad mode="reflect", models.py:23-29) for pads up to 4
 template <int PREC>
@@ -1341,7 +1366,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         }
         float* st1 = stb + A.stash_off[2 * l];
         in_pass(Ti, no_ld, [&](int t, int i, f32x4 yh, f32x4 inv, f32x4) __attribute__((always_inline)) {
-            if (stash) *lz_fl(st1, t, w, i) = yh;
+            if (stash) lz_stash_put<PREC>(st1, t, w, i, yh);
             if (t == c) put_inv(2 * l, inv, i);
             f32x4 v;
 #pragma unroll
@@ -1383,7 +1408,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         // IN over the To frames -> AdaIN(2l+1) -> act -> + (nearest-upsampled) residual
         in_pass(To, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(hin, up == 2 ? t >> 1 : t, w, i)); },
                 [&](int t, int i, f32x4 yh, f32x4 inv, f32x4 res) __attribute__((always_inline)) {
-            if (stash) *lz_fl(st2, t, w, i) = yh;
+            if (stash) lz_stash_put<PREC>(st2, t, w, i, yh);
             if (t == c) put_inv(2 * l + 1, inv, i);
             f32x4 v;
 #pragma unroll
@@ -1574,7 +1599,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     gv[u][i] = gsrc(tc, i);
-                    yv[u][i] = *lz_fl(const_cast<float*>(yq), tc, w, i);
+                    yv[u][i] = lz_stash_get<PREC>(yq, tc, w, i);
                 }
             }
             lz_vm_drain();
@@ -1620,7 +1645,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     zv[u][i] = *lz_fl(tmp, tc, w, i);
-                    yv[u][i] = *lz_fl(const_cast<float*>(yq), tc, w, i);
+                    yv[u][i] = lz_stash_get<PREC>(yq, tc, w, i);
                 }
             }
             lz_vm_drain();
