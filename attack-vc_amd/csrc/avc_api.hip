@@ -54,6 +54,10 @@ __global__ void hdr_compose(HdrArgs A);
 __global__ void hdr_update(HdrArgs A);
 __global__ void pm_conv(PmConvArgs P);
 __global__ void pm_reduce(PmConvArgs P);
+template <int CO>
+__global__ void pm_cin1(PmConvArgs P);
+template <int CI>
+__global__ void pm_cout1(PmConvArgs P);
 template <int MT>
 __global__ void pm_mfma(PmConvArgs P);
 __global__ void vsm_gather(VsmArgs A);

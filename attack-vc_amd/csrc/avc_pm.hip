@@ -151,6 +151,114 @@ __global__ void __launch_bounds__(256) pm_conv(PmConvArgs P) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// The network's two edge layers, whose GEMM shapes waste pm_conv's 64 x 64 tiles: the first
+// (Cin = 1: K = 9) and the last (Cout = 1: one row of 64 used, 98 % of the tile's MACs
+// discarded -- 0.45 ms of a 1.5 ms forward at B = 256).  One thread per output pixel; the
+// per-output arithmetic is pm_conv's: the same fmaf chain over k in pm_conv's K order
+// (ci-major, taps inner), the same K slices summed in slice order as pm_reduce does, then
+// bias + activation -- the results are pm_conv's bit for bit, and batch-invariant.
+// ---------------------------------------------------------------------------------
+// mode 0, Cin = 1, Cout = CO (BN folded, PReLU), NHWC (== NCHW) input, NHWC output: the
+// thread's 9 reflect-gathered inputs, every output channel, staged through LDS so the
+// workgroup's 256 pixels x CO channels (contiguous in NHWC) leave as coalesced 16-byte stores
+template <int CO>
+__global__ void __launch_bounds__(256) pm_cin1(PmConvArgs P) {
+    __shared__ float Ws[CO * 9];
+    __shared__ float Bs[CO];
+    __shared__ float Ys[256 * (CO + 4)];
+    for (int i = threadIdx.x; i < CO * 9; i += 256) Ws[i] = P.w[i];
+    for (int i = threadIdx.x; i < CO; i += 256) Bs[i] = P.bias[i];
+    __syncthreads();
+    const int N = P.B * P.Ho * P.Wo;
+    const int n0 = blockIdx.x * 256, n = n0 + threadIdx.x;
+    if (n < N) {
+        const int b = n / (P.Ho * P.Wo);
+        const int r = n - b * P.Ho * P.Wo;
+        const int oy = r / P.Wo, ox = r - oy * P.Wo;
+        const float* __restrict__ xb = P.x + (size_t)b * P.Hin * P.Win;
+        float xv[9];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                int iy = oy * P.sh + a - 1, ix = ox * P.sw + c - 1;
+                iy = iy < 0 ? -iy : (iy >= P.Hin ? 2 * (P.Hin - 1) - iy : iy);
+                ix = ix < 0 ? -ix : (ix >= P.Win ? 2 * (P.Win - 1) - ix : ix);
+                xv[3 * a + c] = xb[(size_t)iy * P.Win + ix];
+            }
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) acc = fmaf(Ws[co * 9 + k], xv[k], acc);
+            Ys[threadIdx.x * (CO + 4) + co] = pm_act(acc + Bs[co], P);
+        }
+    }
+    __syncthreads();
+    const int nv = min(256, N - n0);
+    f32x4* __restrict__ yo = reinterpret_cast<f32x4*>(P.y + (size_t)n0 * CO);
+    for (int i = threadIdx.x; i < nv * CO / 4; i += 256) {
+        const int px = i / (CO / 4), q = i - px * (CO / 4);
+        yo[i] = *reinterpret_cast<const f32x4*>(&Ys[px * (CO + 4) + 4 * q]);
+    }
+}
+
+// mode 1 (ConvTranspose2d 3x3 stride 2), Cout = 1, NHWC input with CI channels: one thread per
+// output pixel of parity class blockIdx.z; the taps' CI-channel vectors in registers (16-byte
+// loads), then pm_conv's chain; output [B][1][Ho][Wo]
+template <int CI>
+__global__ void __launch_bounds__(256) pm_cout1(PmConvArgs P) {
+    __shared__ float Ws[4 * CI];
+    const int cls = blockIdx.z, py = cls >> 1, px = cls & 1;
+    const int nty = py == 0 ? 2 : 1, ntx = px == 0 ? 2 : 1, nt = nty * ntx;
+    const int K = CI * nt;
+    const float* __restrict__ A = P.w + P.woff[cls];
+    for (int i = threadIdx.x; i < K; i += 256) Ws[i] = A[i];
+    __syncthreads();
+    const int Hq = (P.Ho - py + 1) / 2, Wq = (P.Wo - px + 1) / 2;
+    const int N = P.B * Hq * Wq;
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= N) return;
+    const int b = n / (Hq * Wq);
+    const int r = n - b * Hq * Wq;
+    const int qy = r / Wq, qx = r - qy * Wq;
+    const float* __restrict__ xb = P.x + (size_t)b * CI * P.Hin * P.Win;
+    // tap t of the class: input (qy - a, qx - c) with a = t / ntx, c = t % ntx (py / px = 1: 0)
+    f32x4 xv[4][CI / 4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int a = ntx == 2 ? t >> 1 : t, c = ntx == 2 ? t & 1 : 0;
+        const int iy = py == 0 ? qy - a : qy, ix = px == 0 ? qx - c : qx;
+        const bool ok = t < nt && iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
+        const f32x4* src = reinterpret_cast<const f32x4*>(xb + (size_t)(ok ? iy * P.Win + ix : 0) * CI);
+#pragma unroll
+        for (int q = 0; q < CI / 4; ++q) xv[t][q] = ok ? src[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // pm_conv's K slices (chunks of 16 over k = ci * nt + t; slice edges fall on whole ci) and
+    // pm_reduce's in-order sum of them
+    const int ks = P.ksplit > 1 ? P.ksplit : 1;
+    const int nch = (K + 15) / 16, cps = (nch + ks - 1) / ks;
+    float s = 0.f, acc = 0.f;
+    for (int sl = 0; sl < ks; ++sl) {
+        const int cb = sl * cps * 16 / nt, ce = min(CI, (sl + 1) * cps * 16 / nt);
+        acc = 0.f;
+#pragma unroll
+        for (int ci = 0; ci < CI; ++ci) {
+            if (ci < cb || ci >= ce) continue;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (t < nt) acc = fmaf(Ws[ci * nt + t], xv[t][ci >> 2][ci & 3], acc);
+        }
+        s += acc;
+    }
+    const float v = ks > 1 ? s : acc;
+    const int oy = 2 * qy + py, ox = 2 * qx + px;
+    P.y[((size_t)b * P.Ho + oy) * P.Wo + ox] = pm_act(v + P.bias[0], P);
+}
+template __global__ void pm_cin1<32>(PmConvArgs);
+template __global__ void pm_cout1<32>(PmConvArgs);
+
 // split-K finish: y = act(sum of the K-slice partials in slice order + bias)
 __global__ void __launch_bounds__(256) pm_reduce(PmConvArgs P) {
     const size_t per = (size_t)P.B * P.Cout * P.Ho * P.Wo;

@@ -314,7 +314,7 @@ def main_pm(a):
                        "batch_per_gpu": B, "parallelism": f"dp{world} (independent window shards, no collective)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK["fp32"][0], "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK["fp32"][0], 4), "traffic": None,
-                         "kernel": "pm_conv (whole forward, 12 launches)"},
+                         "kernel": "PredictiveModel forward (pm_cin1, pm_mfma x 10, pm_cout1 + split-K pm_reduce)"},
             "cpu_baseline": cpu, "flop_per_window": FLOP_PER_WINDOW}), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -55,3 +55,19 @@ def test_predictive_rejects_train_mode_and_bad_shapes(pm):
             m(torch.zeros(1, 1, 80, 100, device=DEV))
     finally:
         m.eval()
+
+
+def test_predictive_edge_kernels_bitwise(pm, monkeypatch):
+    """The first (Cin = 1) and last (Cout = 1) layers run on pm_cin1 / pm_cout1, which repeat
+    pm_conv's per-output arithmetic (same fma chain, same K slices summed in order): the whole
+    forward equals the all-pm_conv one (AVC_PM_EDGE=0) bit for bit, odd window shapes included."""
+    z, m = pm
+    g = torch.Generator().manual_seed(12)
+    for shape in ((37, 1, 80, 100), (3, 1, 72, 90)):
+        x = torch.randn(*shape, generator=g).to(DEV)
+        y1 = m(x)
+        monkeypatch.setenv("AVC_PM_EDGE", "0")
+        y0 = m(x)
+        monkeypatch.delenv("AVC_PM_EDGE")
+        torch.cuda.synchronize()
+        assert torch.equal(y0, y1), float((y0 - y1).abs().max())
