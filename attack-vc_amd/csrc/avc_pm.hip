@@ -205,18 +205,19 @@ __global__ void __launch_bounds__(256) pm_cin1(PmConvArgs P) {
 }
 
 // mode 1 (ConvTranspose2d 3x3 stride 2), Cout = 1, NHWC input with CI channels: one thread per
-// output pixel of parity class blockIdx.z; the taps' CI-channel vectors in registers (16-byte
-// loads), then pm_conv's chain; output [B][1][Ho][Wo]
+// 2 x 2 output block (2qy + py, 2qx + px) -- the four parity classes, which together read only
+// the input pixels (qy - {0,1}, qx - {0,1}), loaded once as 16-byte channel vectors -- then per
+// class pm_conv's fma chain over k = ci * nt + t in its K slices, summed in pm_reduce's order.
+// Output [B][1][Ho][Wo]
 template <int CI>
 __global__ void __launch_bounds__(256) pm_cout1(PmConvArgs P) {
-    __shared__ float Ws[4 * CI];
-    const int cls = blockIdx.z, py = cls >> 1, px = cls & 1;
-    const int nty = py == 0 ? 2 : 1, ntx = px == 0 ? 2 : 1, nt = nty * ntx;
-    const int K = CI * nt;
-    const float* __restrict__ A = P.w + P.woff[cls];
-    for (int i = threadIdx.x; i < K; i += 256) Ws[i] = A[i];
+    __shared__ float Ws[4][4 * CI];
+    for (int c = 0; c < 4; ++c) {
+        const int K = CI * ((c >> 1) == 0 ? 2 : 1) * ((c & 1) == 0 ? 2 : 1);
+        for (int i = threadIdx.x; i < K; i += 256) Ws[c][i] = P.w[P.woff[c] + i];
+    }
     __syncthreads();
-    const int Hq = (P.Ho - py + 1) / 2, Wq = (P.Wo - px + 1) / 2;
+    const int Hq = (P.Ho + 1) / 2, Wq = (P.Wo + 1) / 2;   // class (0, 0): the most blocks
     const int N = P.B * Hq * Wq;
     const int n = blockIdx.x * 256 + threadIdx.x;
     if (n >= N) return;
@@ -224,37 +225,48 @@ __global__ void __launch_bounds__(256) pm_cout1(PmConvArgs P) {
     const int r = n - b * Hq * Wq;
     const int qy = r / Wq, qx = r - qy * Wq;
     const float* __restrict__ xb = P.x + (size_t)b * CI * P.Hin * P.Win;
-    // tap t of the class: input (qy - a, qx - c) with a = t / ntx, c = t % ntx (py / px = 1: 0)
-    f32x4 xv[4][CI / 4];
+    // xv[dy][dx] = input (qy - dy, qx - dx), zero outside
+    f32x4 xv[2][2][CI / 4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const int a = ntx == 2 ? t >> 1 : t, c = ntx == 2 ? t & 1 : 0;
-        const int iy = py == 0 ? qy - a : qy, ix = px == 0 ? qx - c : qx;
-        const bool ok = t < nt && iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
-        const f32x4* src = reinterpret_cast<const f32x4*>(xb + (size_t)(ok ? iy * P.Win + ix : 0) * CI);
+    for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
-        for (int q = 0; q < CI / 4; ++q) xv[t][q] = ok ? src[q] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    // pm_conv's K slices (chunks of 16 over k = ci * nt + t; slice edges fall on whole ci) and
-    // pm_reduce's in-order sum of them
-    const int ks = P.ksplit > 1 ? P.ksplit : 1;
-    const int nch = (K + 15) / 16, cps = (nch + ks - 1) / ks;
-    float s = 0.f, acc = 0.f;
-    for (int sl = 0; sl < ks; ++sl) {
-        const int cb = sl * cps * 16 / nt, ce = min(CI, (sl + 1) * cps * 16 / nt);
-        acc = 0.f;
+        for (int dx = 0; dx < 2; ++dx) {
+            const int iy = qy - dy, ix = qx - dx;
+            const bool ok = iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
+            const f32x4* src = reinterpret_cast<const f32x4*>(xb + (size_t)(ok ? iy * P.Win + ix : 0) * CI);
 #pragma unroll
-        for (int ci = 0; ci < CI; ++ci) {
-            if (ci < cb || ci >= ce) continue;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (t < nt) acc = fmaf(Ws[ci * nt + t], xv[t][ci >> 2][ci & 3], acc);
+            for (int q = 0; q < CI / 4; ++q) xv[dy][dx][q] = ok ? src[q] : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        s += acc;
+    const int ks = P.ksplit > 1 ? P.ksplit : 1;
+#pragma unroll
+    for (int cls = 0; cls < 4; ++cls) {
+        const int py = cls >> 1, px = cls & 1;
+        const int oy = 2 * qy + py, ox = 2 * qx + px;
+        if (oy >= P.Ho || ox >= P.Wo) continue;
+        const int nty = py == 0 ? 2 : 1, ntx = px == 0 ? 2 : 1, nt = nty * ntx;
+        const int K = CI * nt;
+        const int nch = (K + 15) / 16, cps = (nch + ks - 1) / ks;
+        float s = 0.f, acc = 0.f;
+        for (int sl = 0; sl < ks; ++sl) {
+            const int cb = sl * cps * 16 / nt, ce = min(CI, (sl + 1) * cps * 16 / nt);
+            acc = 0.f;
+#pragma unroll
+            for (int ci = 0; ci < CI; ++ci) {
+                if (ci < cb || ci >= ce) continue;
+                // tap t = a * ntx + c reads input (qy - a [py = 0], qx - c [px = 0])
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (t >= nt) continue;
+                    const int ta = ntx == 2 ? t >> 1 : t, tc = ntx == 2 ? t & 1 : 0;
+                    const int dy = py == 0 ? ta : 0, dx = px == 0 ? tc : 0;
+                    acc = fmaf(Ws[cls][ci * nt + t], xv[dy][dx][ci >> 2][ci & 3], acc);
+                }
+            }
+            s += acc;
+        }
+        const float v = ks > 1 ? s : acc;
+        P.y[((size_t)b * P.Ho + oy) * P.Wo + ox] = pm_act(v + P.bias[0], P);
     }
-    const float v = ks > 1 ? s : acc;
-    const int oy = 2 * qy + py, ox = 2 * qx + px;
-    P.y[((size_t)b * P.Ho + oy) * P.Wo + ox] = pm_act(v + P.bias[0], P);
 }
 template __global__ void pm_cin1<32>(PmConvArgs);
 template __global__ void pm_cout1<32>(PmConvArgs);
