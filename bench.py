@@ -588,6 +588,13 @@ def main():
             "flop_per_utt_iter": fl,
             "tflops_whole_step": round(fl * a.n_iters * total * a.steps / elapsed / 1e12, 2),
         }
+        if roof is not None:
+            # the unprofiled graph-replayed loop's algorithmic rate over the peak, next to the
+            # per-kernel (HIP-event, instrumented) frac above: the in-loop figure has no profiler
+            # stretch, and the per-kernel times summed exceed ms_per_step / n_iters by that stretch
+            pk = PEAK[a.precision][0]
+            roof["frac_in_loop_whole_step"] = round(line["tflops_whole_step"] / world / pk, 4)
+            roof["iter_ms_in_loop"] = round(ms / a.n_iters, 5)
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
