@@ -538,25 +538,42 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         }
     }
     // ContentEncoder: h0 = act(IN(in_conv + b)) (models.py:195-200)
-    auto in_apply = [&](int Tl, auto&& out) __attribute__((always_inline)) {
+    // (LZ_FB fragments at a time: their loads -- raw and ex = ld(t, i), the residual or nothing --
+    // then one drain, then the stores; as the decoder's in_pass)
+    auto in_apply = [&](int Tl, auto&& ld, auto&& out) __attribute__((always_inline)) {
         lz_publish();
         f32x4 mean[2], inv[2];
         lz_in_stats(raw, Tl, w, in_s, mean, inv);
-        for (int F = 0; F < lz_nf(Tl); ++F) {
-            const int t = 16 * F + c;
-            if (t < Tl)
+        for (int F0 = 0; F0 < lz_nf(Tl); F0 += LZ_FB) {
+            f32x4 rv[LZ_FB][2], ex[LZ_FB][2];
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int tc = min(16 * (F0 + u) + c, Tl - 1);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    f32x4 v = (*lz_fl(raw, t, w, i) - mean[i]) * inv[i];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = act_f(v[r], act);
-                    out(t, i, v);
+                    rv[u][i] = *lz_fl(raw, tc, w, i);
+                    ex[u][i] = ld(tc, i);
                 }
+            }
+            lz_vm_drain();
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int t = 16 * (F0 + u) + c;
+                if (t < Tl)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        f32x4 v = (rv[u][i] - mean[i]) * inv[i];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = act_f(v[r], act);
+                        out(t, i, v, ex[u][i]);
+                    }
+            }
         }
         in_s[0] = in_s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
+    auto no_ld = [](int, int) __attribute__((always_inline)) { return f32x4{0.f, 0.f, 0.f, 0.f}; };
     if (ce)
-        in_apply(T, [&](int t, int i, f32x4 v) __attribute__((always_inline)) {
+        in_apply(T, no_ld, [&](int t, int i, f32x4 v, f32x4) __attribute__((always_inline)) {
             *lz_fl(hf[0], t, w, i) = v;
             lz_put<PREC>(imgh, t, T, (ch0 + 16 * i) * ESZ, v);
         });
@@ -620,7 +637,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             FZ_PH();
         }
         if (ce)
-            in_apply(Ti, [&](int t, int i, f32x4 v) __attribute__((always_inline)) {
+            in_apply(Ti, no_ld, [&](int t, int i, f32x4 v, f32x4) __attribute__((always_inline)) {
                 lz_put<PREC>(imgy, t, Ti, (ch0 + 16 * i) * ESZ, v);
             });
         lz_publish();                                   // imgy complete
@@ -629,7 +646,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         float* hin = hf[cur];
         float* hout = hf[cur ^ 1];
         const int nfo = lz_nf(To);
-        auto pool = [&](int t, int i) __attribute__((always_inline)) {
+        auto pool = [&](int t, int i) __attribute__((always_inline)) -> f32x4 {
             if (s == 1) return *lz_fl(hin, t, w, i);
             const f32x4 a = *lz_fl(hin, 2 * t, w, i);
             if (2 * t + 1 < Ti) return (a + *lz_fl(hin, 2 * t + 1, w, i)) / 2.f;
@@ -706,8 +723,8 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
             FZ_PH();
         }
         if (ce)
-            in_apply(To, [&](int t, int i, f32x4 v) __attribute__((always_inline)) {
-                const f32x4 h = v + pool(t, i);
+            in_apply(To, pool, [&](int t, int i, f32x4 v, f32x4 pv) __attribute__((always_inline)) {
+                const f32x4 h = v + pv;
                 *lz_fl(hout, t, w, i) = h;
                 lz_put<PREC>(imgh, t, To, (ch0 + 16 * i) * ESZ, h);
             });
