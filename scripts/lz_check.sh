@@ -1,6 +1,8 @@
 #!/bin/bash
 # Long-engine iteration: GPU tests of the long / generic-length paths, an interleaved A/B of the
-# T=400 emb attack against scripts/dbg/var/base, and the phase stamps of scripts/dbg/phl.
+# T=400 emb attack against scripts/dbg/var/base (build it from an older checkout with
+# scripts/dbg/build_var.sh base "" avc_long.hip, or name other variants in LZ_VARS), and the phase
+# stamps of scripts/dbg/phl (scripts/dbg/build_phases_long.sh) when built.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest ${LZ_TESTS:-tests/test_gpu_long.py tests/test_gpu_lengths.py tests/test_gpu_lrelu.py} -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/lz_tests.log 2>&1
