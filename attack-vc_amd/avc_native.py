@@ -118,9 +118,9 @@ SIGNATURES = [
                                       ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_pm_block_shape", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
-                                          ctypes.POINTER(ctypes.c_int)]),
+                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     ("avc_pm_block_forward", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_vsmask_windows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     ("avc_vsmask_protect", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
@@ -649,13 +649,16 @@ class PMContext:
         if x.dim() != 4:
             raise RuntimeError(f"expected [B, C, H, W], got {tuple(x.shape)}")
         B, C, H, W = x.shape
-        c, ho, wo = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        c, ho, wo, cin = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _check(lib().avc_pm_block_shape(self.h, int(layer), int(H), int(W), ctypes.byref(c), ctypes.byref(ho),
-                                        ctypes.byref(wo)))
+                                        ctypes.byref(wo), ctypes.byref(cin)))
+        if C != cin.value:   # torch's Conv2d / ConvTranspose2d shape error (the C ABI refuses it too)
+            raise RuntimeError(f"PredictiveModel block {layer}: expected input[{B}, {cin.value}, {H}, {W}], "
+                               f"got {C} channels")
         y = torch.empty(B, c.value, ho.value, wo.value, device=x.device, dtype=torch.float32)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         with self._lock:
-            _check(lib().avc_pm_block_forward(self.h, int(layer), ctypes.c_void_p(x.data_ptr()), B, H, W,
+            _check(lib().avc_pm_block_forward(self.h, int(layer), ctypes.c_void_p(x.data_ptr()), B, C, H, W,
                                               ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(stream)))
         return y
 

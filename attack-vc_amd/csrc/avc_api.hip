@@ -1350,6 +1350,16 @@ static int alloc_long(LongArgs& L, int B, int T, int nlayers) {
 }
 
 // a workspace whose build failed part-way: release what it holds and forget it (returns 1)
+static int drop_ws(avc_ctx* ctx);
+// HIPCHK for a workspace under construction: on failure the half-built entry is dropped (drop_ws)
+#define WSCHK(expr)                                                                                   \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) {                                                                   \
+            fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__);      \
+            return drop_ws(ctx);                                                                  \
+        }                                                                                         \
+    } while (0)
 static int drop_ws(avc_ctx* ctx) {
     for (auto it = ctx->wss.begin(); it != ctx->wss.end(); ++it)
         if (&*it == ctx->cur) {
@@ -1439,7 +1449,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
             rc |= dalloc(ws.gpooled, (size_t)B * FZ_C);
             rc |= dalloc(ws.loss_cur, (size_t)B);
             if (rc) return drop_ws(ctx);
-            HIPCHK(hipMalloc(&ws.masks, (size_t)B * ws.mask_words * sizeof(unsigned long long)));
+            WSCHK(hipMalloc(&ws.masks, (size_t)B * ws.mask_words * sizeof(unsigned long long)));
             if (ws.lz && alloc_long(ws.lza, B, T, nb + 1 + 2 * c.n_conv_blocks)) return drop_ws(ctx);
         } else {
             rc |= dalloc(ws.gxd, X);
@@ -1458,7 +1468,7 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
             rc |= dalloc(ws.slab, (size_t)KSPLIT_MAX * std::max(c.c_h, c.c_in) * B * T);
         }
         if (rc) return drop_ws(ctx);
-        HIPCHK(hipMalloc(&ws.step, sizeof(int)));
+        WSCHK(hipMalloc(&ws.step, sizeof(int)));
         if (dalloc(ws.scal, 8)) return drop_ws(ctx);
     } else {
         ++ctx->n_ws_replans;   // more iterations than this workspace's tables hold
@@ -1479,8 +1489,8 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
     if (plan_iteration(ctx, ws, ws.iter, PREC_F32)) return drop_ws(ctx);
     // autotune with a valid Adam step (1) and eps/gscale (the kernels clamp anyway)
     const float scal0[8] = {0.1f, 0.f, 0.f, 0.f, 0.1f, 0.f, 0.f, 0.f};
-    HIPCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(ws.step, 0, sizeof(int)));
+    WSCHK(hipMemcpy(ws.scal.p, scal0, sizeof(scal0), hipMemcpyHostToDevice));
+    WSCHK(hipMemset(ws.step, 0, sizeof(int)));
     if (autotune(ctx, ws.fwd) || autotune(ctx, ws.iter)) return drop_ws(ctx);
     ws.built = true;
     return 0;

@@ -208,9 +208,12 @@ int avc_pm_forward(avc_pm* pm, const float* x, int B, int H, int W, float* y, vo
 /* One block of the network on its own: layer 0..6 = down_blocks.0..6 (DownSamplingBlock.forward,
  * models/predictive_model.py:28-29), 7..11 = up_blocks.0..4 (UpSamplingBlock.forward, 50-51; the final
  * tanh is PredictiveModel.forward's, not the block's).  x [B][Cin][H][W] -> y [B][C][Ho][Wo] (NCHW,
- * device); avc_pm_block_shape gives C, Ho, Wo (non-zero if the input is too small). */
-int avc_pm_block_shape(avc_pm* pm, int layer, int H, int W, int* C, int* Ho, int* Wo);
-int avc_pm_block_forward(avc_pm* pm, int layer, const float* x, int B, int H, int W, float* y, void* stream);
+ * device); avc_pm_block_shape gives C, Ho, Wo (non-zero if the input is too small) and, if Cin is
+ * non-NULL, the layer's input channel count.  avc_pm_block_forward fails unless Cin equals the layer's
+ * (torch's Conv2d shape check: the kernel would otherwise read B*Cin_layer*H*W floats of x). */
+int avc_pm_block_shape(avc_pm* pm, int layer, int H, int W, int* C, int* Ho, int* Wo, int* Cin);
+int avc_pm_block_forward(avc_pm* pm, int layer, const float* x, int B, int Cin, int H, int W, float* y,
+                         void* stream);
 
 /* ---- VSMask protect loop (/root/reference/vsmask.py:160-213, utils/audio.py:77-116,
  * models/header_model.py:70-95) ----

@@ -152,9 +152,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--skip-1500", action="store_true")
-    ap.add_argument("--stage", default="all", choices=["all", "base", "long"],
+    ap.add_argument("--stage", default="all", choices=["all", "base", "long", "long100"],
                     help="long: only the round-2 fixtures (T = 300 with three input lengths; "
-                         "e2e / fb at n = 100)")
+                         "e2e / fb at n = 100); long100: only full_T300_n100.npz (round 4)")
     a = ap.parse_args()
     sys.dont_write_bytecode = True
     sys.path.insert(0, a.ref)
@@ -165,7 +165,9 @@ def main():
 
     if a.stage in ("all", "long"):
         long_fixtures(models, au, seeds)
-    if a.stage == "long":
+    if a.stage in ("all", "long100"):
+        long100_fixtures(models, au, seeds)
+    if a.stage in ("long", "long100"):
         return
 
     # ---------------- small config -------------------------------------------------
@@ -254,6 +256,25 @@ def long_fixtures(models, au, seeds):
     for kind in ("e2e", "fb"):
         attack_fixture(au, kind, model, X, [100], seeds, "", out, keep_losses=True)
     path = os.path.join(HERE, "full_T128_n100.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path))
+
+
+def long100_fixtures(models, au, seeds):
+    """Round 4: full_T300_n100.npz -- full_T300.npz's inputs (vc_src 280, vc_tgt 300, adv_tgt 260
+    frames, seed 300) attacked for 100 iterations by emb / e2e / fb: adv at n = 100, grad0 and the
+    whole loss history (the long engine at the horizon of SURVEY 8(c)'s n = 100 tolerance)."""
+    model = build(models, FULL_CFG)
+    hashes = {k: sha(v) for k, v in model.state_dict().items()}
+    X = make_inputs(2, {"vc_src": 280, "vc_tgt": 300, "adv_tgt": 260}, seed=300)
+    out = {"config": np.array(json.dumps(FULL_CFG)), "eps": np.float64(EPS), "T": np.int64(300),
+           "weight_sha256": np.array(json.dumps(hashes))}
+    for kind in ("emb", "e2e", "fb"):
+        attack_fixture(au, kind, model, X, [100], seeds, "", out, keep_losses=True)
+    for k in list(out):   # the inputs and targets live in full_T300.npz (same seed); keep vectors only
+        if k.endswith(("_org", "_tgt")) and not k.startswith(("vc_", "adv_")):
+            del out[k]
+    path = os.path.join(HERE, "full_T300_n100.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path))
 

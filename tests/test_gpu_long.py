@@ -6,7 +6,8 @@ kernels family with the activations chunked through global scratch.
     and the reference's own golden vectors (tests/golden/full_T128.npz) are reproduced;
   * T in {129, 200, 257, 600} (AUTO picks "long" above 128): SpeakerEncoder(x), the emb
     attack's iteration-0 gradient and 10-iteration adv against the float64 oracle;
-  * a reference-generated golden at T = 300 (tests/golden/full_T300.npz);
+  * reference-generated goldens at T = 300 (tests/golden/full_T300.npz at n = 10,
+    full_T300_n100.npz at n = 100);
   * bf16 vs fp32, determinism and shard invariance at T = 300."""
 import os
 
@@ -160,6 +161,23 @@ def test_long_vc_golden_T300(full, golden, kind):
     check_adv(adv.detach().cpu().numpy(), zl[f"{kind}_adv_n10"], 10)
     assert rel(info["grad0"].cpu().numpy(), zl[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
     np.testing.assert_allclose(info["losses"].cpu().numpy().T, zl[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("kind", ["emb", "e2e", "fb"])
+def test_long_golden_T300_n100(full, golden, kind):
+    """The reference's own 100-iteration attacks at vc_src 280 / vc_tgt 300 / adv_tgt 260 frames
+    (tests/golden/full_T300_n100.npz, make_golden.py --stage long100): the long engine at the
+    SURVEY 8(c) n = 100 fp32 tolerances (adv max 1e-3 / mean 1e-6), grad0 and the whole loss
+    history (rtol 2e-4)."""
+    zl, zn = golden("full_T300"), golden("full_T300_n100")
+    z, m, ctx, _ = full
+    fn = {"emb": attack_utils.emb_attack, "e2e": attack_utils.e2e_attack, "fb": attack_utils.fb_attack}[kind]
+    args = (_dev(zl["vc_tgt"]), _dev(zl["adv_tgt"])) if kind == "emb" else \
+        (_dev(zl["vc_src"]), _dev(zl["vc_tgt"]), _dev(zl["adv_tgt"]))
+    adv, info = fn(m, *args, 0.1, 100, ptb0=_dev(zn[f"{kind}_ptb0"]), return_info=True)
+    check_adv(adv.detach().cpu().numpy(), zn[f"{kind}_adv_n100"], 100)
+    assert rel(info["grad0"].cpu().numpy(), zn[f"{kind}_grad0"]) <= (TOL_GRAD_REL if kind == "emb" else TOL_GRAD_REL_VC)
+    np.testing.assert_allclose(info["losses"].cpu().numpy().T, zn[f"{kind}_losses_n100"], rtol=2e-4, atol=1e-9)
 
 
 def test_long_inference_golden_T300(full, golden):

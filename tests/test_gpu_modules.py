@@ -2,6 +2,8 @@
 the reference's own outputs (tests/golden/modules.npz, make_modules.py):
 ContentEncoder.forward -> (mu, log_sigma) (/root/reference/models.py:181-210), Decoder.forward
 (403-435), each on the fused (T <= 128) and the long engine."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -93,3 +95,19 @@ def test_predictive_blocks_forward(golden):
     full = pm(x)
     assert full.shape == chain.shape
     assert float((torch.tanh(chain) - full).abs().max()) <= 1e-4
+
+
+def test_predictive_block_wrong_channels():
+    """A block fed the wrong channel count raises like torch's Conv2d shape check instead of reading
+    past the input (the C ABI checks Cin too)."""
+    import avc_native
+    import predictive_model
+    torch.manual_seed(0)
+    pm = predictive_model.PredictiveModel().eval().to(DEV)
+    ctx = avc_native.pm_context_for(pm, DEV)
+    with pytest.raises(RuntimeError, match="channels"):
+        pm.down_blocks[3](torch.zeros(1, 32, 20, 13, device=DEV))
+    x = torch.zeros(1, 32, 20, 13, device=DEV)
+    rc = avc_native.lib().avc_pm_block_forward(ctx.h, 3, ctypes.c_void_p(x.data_ptr()), 1, 32, 20, 13,
+                                               ctypes.c_void_p(x.data_ptr()), None)
+    assert rc != 0 and b"channels" in avc_native.lib().avc_last_error()

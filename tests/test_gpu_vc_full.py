@@ -4,7 +4,9 @@
     by attack_utils.e2e_attack / fb_attack on CPU from full_T128.npz's inputs) -- adv at the
     SURVEY 8(c) fp32 tolerances for n = 100 (max 1e-3, mean 1e-6), grad0 and the whole loss
     history at rtol 2e-4;
-  * configs[2] / configs[3]'s own size, B = 256 and T = 128 (the bench workload): determinism,
+  * configs[3] at its full size on the one GPU: B = 2048 fb over 8 shard contexts (bitwise vs the
+    shards attacked alone, loss decrease, two utterances vs the float64 oracle);
+  * configs[2] / configs[3]'s per-GPU size, B = 256 and T = 128 (the bench workload): determinism,
     the perturbation bound |adv - vc| <= eps, the per-utterance loss decreasing, and two utterances of
     the batch spot-checked against the float64 oracle over 50 iterations -- in fp32, then the
     same properties in the bench's bf16 mode plus the SURVEY 8(c) bf16 adv bound.
@@ -81,3 +83,44 @@ def test_vc_full_size_properties(full, kind):
     L16 = info16["losses"].cpu().numpy()
     assert np.all(L16[-1] < L16[0]), int(np.sum(L16[-1] >= L16[0]))
     assert float((a16 - a).abs().max()) <= 2e-2            # SURVEY 8(c) bf16 adv bound (n <= 100)
+
+
+def test_configs3_fb_b2048_on_one_gpu(full):
+    """configs[3] at its own size: B = 2048 fb attack at T = 128 in bf16, sharded 8 ways through
+    shard.attack_multi_gpu -- 8 model replicas, hence 8 libavc contexts and 8 host threads, all on
+    the box's one GPU (the 8-GPU path with the devices folded onto cuda:0).  n = 20.
+      * bitwise equal to the 8 shards attacked one after the other on a single context;
+      * |adv - vc| <= eps everywhere, every utterance's loss decreased;
+      * two utterances against the float64 oracle: the bf16 result within SURVEY 8(c)'s bf16 bound,
+        and the same two attacked in fp32 within its n = 100 fp32 tolerances."""
+    import copy
+
+    import shard
+    z, m = full
+    B, T, n, G = 2048, 128, 20, 8
+    g = torch.Generator().manual_seed(2048)
+    src, vc, at = (torch.randn(B, 80, T, generator=g) for _ in range(3))
+    p0 = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(123))
+    reps = [copy.deepcopy(m) for _ in range(G)]
+    out = shard.attack_multi_gpu("fb", reps, src.to(DEV), vc.to(DEV), at.to(DEV), 0.1, n, ptb0=p0.to(DEV),
+                                 precision="bf16").detach()
+    assert out.shape == (B, 80, T)
+    assert float((out - vc.to(DEV)).abs().max()) <= 0.1 + 1e-6
+    for i in range(G):
+        sl = shard.shard_slice(B, i, G)
+        o, info = attack_utils.fb_attack(m, src[sl].to(DEV), vc[sl].to(DEV), at[sl].to(DEV), 0.1, n,
+                                         ptb0=p0[sl].to(DEV), precision="bf16", return_info=True)
+        assert torch.equal(o.detach(), out[sl]), i
+        L = info["losses"].cpu().numpy()               # [n, 256]
+        assert np.all(L[-1] < L[0]), (i, int(np.sum(L[-1] >= L[0])))
+    del reps
+    idx = [5, B - 3]                                    # one utterance each of shards 0 and 7
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    w64 = oracle.Weights(sd, dtype=np.float64)
+    f64 = [t[idx].numpy().astype(np.float64) for t in (src, vc, at, p0)]
+    ref = oracle.fb_attack(w64, cfg_of(z), *f64[:3], 0.1, n, f64[3])
+    d16 = np.abs(out[idx].cpu().numpy().astype(np.float64) - ref)
+    assert d16.max() <= 2e-2, d16.max()
+    a32 = attack_utils.fb_attack(m, *(t[idx].to(DEV) for t in (src, vc, at)), 0.1, n, ptb0=p0[idx].to(DEV)).detach()
+    d32 = np.abs(a32.cpu().numpy().astype(np.float64) - ref)
+    assert d32.max() <= 1e-3 and d32.mean() <= 1e-6, (d32.max(), d32.mean())
