@@ -26,11 +26,20 @@ TOL_GRAD_REL_VC = 1e-3
 # utterances agree to ~5e-6.  So: every utterance <= 5e-3, the median <= 2e-5.
 TOL_VC_GRAD_L2_MAX = 5e-3
 TOL_VC_GRAD_L2_MEDIAN = 2e-5
-# Adam divides each element's step by that element's own gradient RMS, so an
-# element whose gradient nearly cancels amplifies last-bit differences in the
-# summation order: the max is loose, the mean is the sharp check.
-TOL_ADV = {1: 1e-5, 10: 1e-4, 100: 1e-3, 1500: 5e-3}
-TOL_ADV_MEAN = {1: 1e-8, 10: 1e-7, 100: 1e-6, 1500: 1e-4}
+# adv vs the reference's own fp32 run.  Calibrated in round 4 (profiles/r04/tol_calibration.md,
+# scripts/tol_calibration.py) against the reference's float64 run of the same attacks
+# (tests/golden/calib_f64_T128.npz): at n = 1 every engine is within one fp32 ulp of the golden; by
+# n = 10 a differently ordered fp32 sum may flip a ReLU whose pre-activation is within rounding of
+# zero, which changes the gradient over that unit's receptive field only (one window of ~12 frames
+# of one utterance), and where |grad| < Adam's eps (1e-8; the attacks' gradients are ~1e-8) the step
+# is linear in the gradient (lr / eps = 1e5 amplification): the fused engine's 6.2e-6 at n = 10 sits
+# on 34 elements, all with |grad| <= 2.5e-8, in frames 76-87 of one utterance.  The reference's own
+# fp32 run shows the same mechanism by n = 100 (1.0e-5 vs float64, in the same frame windows).  The
+# bounds are ~3x the largest distance any GPU test measured (AVC_TOL_LOG, profiles/r04/tol_log.json):
+# max 2.4e-7 / 1.6e-5 / 3.3e-5 / 6.1e-5 and mean 2.3e-9 / 8.9e-8 / 2.1e-7 / 1.4e-6 at n = 1 / 10 / 100 /
+# 1500; SURVEY 8(c)'s n = 100 / 1500 bounds are met with room (1e-4; 5e-3, mean 1e-4).
+TOL_ADV = {1: 1e-6, 10: 5e-5, 100: 1e-4, 1500: 5e-4}
+TOL_ADV_MEAN = {1: 1e-8, 10: 1e-7, 100: 1e-6, 1500: 5e-6}
 
 
 def check_grad_flip_robust(g, ref, frac=0.05):

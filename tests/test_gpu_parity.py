@@ -6,7 +6,7 @@ import torch
 
 import attack_utils
 import avc_native
-from helpers import TOL_GRAD_REL, TOL_SE_REL, cfg_of, check_adv, model_from_fixture, oracle_weights, rel
+from helpers import TOL_ADV, TOL_GRAD_REL, TOL_SE_REL, cfg_of, check_adv, model_from_fixture, oracle_weights, rel
 from oracle import adain_vc as oracle
 
 pytestmark = pytest.mark.gpu
@@ -236,3 +236,26 @@ def test_pgd_update_matches_restatement(gpu, golden):
     ref = pgd_attack_np(oracle_weights(m), cfg_of(z), z["vc_tgt"], z["adv_tgt"], 0.1, 20, z["emb_ptb0"], 5e-3)
     d = np.abs(a - ref)
     assert np.mean(d <= 1e-5) >= 0.99, np.mean(d <= 1e-5)
+
+
+def test_fp32_error_sits_on_near_zero_gradients(gpu, golden):
+    """The fp32 tolerance calibration (tests/helpers.py TOL_ADV; profiles/r04/tol_calibration.md) as a
+    test: the fused emb attack at n = 10 vs the reference's float64 run (calib_f64_T128.npz, made by
+    tests/golden/make_calib.py) -- within TOL_ADV[10], mean at the reference's own fp32 level, and every
+    element off by more than 3e-6 has |d loss / d ptb| below Adam's eps (1e-8: the regime where the
+    step is linear in the gradient) and lies in one window of <= 16 frames of its utterance (the
+    receptive field of a ReLU that flipped), not spread over the mel."""
+    z, zf = golden("full_T128"), golden("calib_f64_T128")
+    m = model_from_fixture(z).to(gpu)
+    adv = attack_utils.emb_attack(m, _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
+                                  ptb0=_dev(z["emb_ptb0"])).detach().cpu().numpy().astype(np.float64)
+    d = np.abs(adv - zf["emb_adv_n10"])
+    assert d.max() <= TOL_ADV[10], d.max()
+    assert d.mean() <= 5e-8, d.mean()
+    big = d > 3e-6
+    if big.any():
+        assert np.abs(zf["emb_grad0"])[big].max() < 1e-8
+        for b in range(d.shape[0]):
+            fr = np.where(big[b].any(0))[0]
+            if fr.size:
+                assert fr.max() - fr.min() < 16, (b, fr)

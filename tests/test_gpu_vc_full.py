@@ -90,7 +90,8 @@ def test_configs3_fb_b2048_on_one_gpu(full):
     shard.attack_multi_gpu -- 8 model replicas, hence 8 libavc contexts and 8 host threads, all on
     the box's one GPU (the 8-GPU path with the devices folded onto cuda:0).  n = 20.
       * bitwise equal to the 8 shards attacked one after the other on a single context;
-      * |adv - vc| <= eps everywhere, every utterance's loss decreased;
+      * |adv - vc| <= eps everywhere; every utterance's fp32 objective decreased (and >= 99 % of
+        the bf16 loss histories);
       * two utterances against the float64 oracle: the bf16 result within SURVEY 8(c)'s bf16 bound,
         and the same two attacked in fp32 within its n = 100 fp32 tolerances."""
     import copy
@@ -106,13 +107,25 @@ def test_configs3_fb_b2048_on_one_gpu(full):
                                  precision="bf16").detach()
     assert out.shape == (B, 80, T)
     assert float((out - vc.to(DEV)).abs().max()) <= 0.1 + 1e-6
+    dec = 0
     for i in range(G):
         sl = shard.shard_slice(B, i, G)
         o, info = attack_utils.fb_attack(m, src[sl].to(DEV), vc[sl].to(DEV), at[sl].to(DEV), 0.1, n,
                                          ptb0=p0[sl].to(DEV), precision="bf16", return_info=True)
         assert torch.equal(o.detach(), out[sl]), i
-        L = info["losses"].cpu().numpy()               # [n, 256]
-        assert np.all(L[-1] < L[0]), (i, int(np.sum(L[-1] >= L[0])))
+        L = info["losses"].cpu().numpy()               # [n, 256], the bf16 objective
+        dec += int(np.sum(L[-1] < L[0]))
+    # the bf16 objective's own rounding is comparable to 20 steps of progress for a few utterances,
+    # so every utterance's decrease is asserted on the fp32 objective (one fp32 evaluation at the
+    # initial and at the final adversarial mel: ptb recovered as atanh((adv - vc) / eps) in float64)
+    assert dec >= 0.99 * B, dec
+    y = ((out.cpu().double() - vc.double()) / 0.1).clamp(-1 + 1e-7, 1 - 1e-7)
+    p1 = torch.atanh(y).float()
+    l0 = attack_utils.fb_attack(m, src.to(DEV), vc.to(DEV), at.to(DEV), 0.1, 1, ptb0=p0.to(DEV),
+                                return_info=True)[1]["losses"][0].cpu().numpy()
+    l1 = attack_utils.fb_attack(m, src.to(DEV), vc.to(DEV), at.to(DEV), 0.1, 1, ptb0=p1.to(DEV),
+                                return_info=True)[1]["losses"][0].cpu().numpy()
+    assert np.all(l1 < l0), (int(np.sum(l1 >= l0)), float(np.max((l1 - l0) / np.abs(l0))))
     del reps
     idx = [5, B - 3]                                    # one utterance each of shards 0 and 7
     sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
