@@ -33,10 +33,6 @@ __global__ void se_fwd_fused(FusedArgs A);
 template <int PREC, int SH>
 __global__ void se_bwd_fused(FusedArgs A);
 template <int PREC>
-__global__ void se_fwd8(FusedArgs A);
-template <int PREC>
-__global__ void se_bwd8(FusedArgs A);
-template <int PREC>
 __global__ void lz_se_fwd(FusedArgs A, LongArgs L);
 template <int PREC>
 __global__ void lz_se_bwd(FusedArgs A, LongArgs L);
@@ -141,7 +137,6 @@ struct Launch {
     FusedArgs fz{};              // L_FZ_* / L_LZ_*: per-utterance SpeakerEncoder pass (prec = PREC_*)
     LongArgs lz{};               // L_LZ_*: the long engine's scratch
     int fz_shape = 8;            // L_FZ_*: kernel shape SH (0 = standard config at T = 128, else 1|2|4|8)
-    bool fz8 = false;            // L_FZ_* bf16 shape 0: the 8-wave kernels (avc_fused8.hip)
     DecArgs dz{};                // L_DZ_*: per-utterance fused Decoder pass (shape: fz_shape 0 | 8)
     DenseArgs dn{};              // L_DENSE: batched conv_affine layer (or its transpose)
     HdrArgs hd{};                // L_HDR_*: the header optimiser's elementwise ends
@@ -458,17 +453,13 @@ static int set_fused_attrs() {
     // every fused kernel needs more than the default 64 KiB of dynamic LDS
 #define AVC_FZ_FNS(SH)                                                                      \
     {(const void*)se_fwd_fused<PREC_F32, SH>, fz_lds_fwd(PREC_F32, 128, 5)},                \
-        {(const void*)se_fwd_fused<PREC_BF16, SH>, fz_lds_fwd(PREC_BF16, 128, 5)},          \
+        {(const void*)se_fwd_fused<PREC_BF16, SH>, fz_lds_fwd(PREC_BF16, 128, 5)},   \
         {(const void*)se_bwd_fused<PREC_F32, SH>, fz_lds_bwd(PREC_F32, 128)},                \
         {(const void*)se_bwd_fused<PREC_BF16, SH>, fz_lds_bwd(PREC_BF16, 128)}
     const std::pair<const void*, int> fns[] = {AVC_FZ_FNS(0), AVC_FZ_FNS(1), AVC_FZ_FNS(2), AVC_FZ_FNS(4),
                                                AVC_FZ_FNS(8)};
 #undef AVC_FZ_FNS
     for (auto& fn : fns) HIPCHK(hipFuncSetAttribute(fn.first, hipFuncAttributeMaxDynamicSharedMemorySize, fn.second));
-    HIPCHK(hipFuncSetAttribute((const void*)se_fwd8<PREC_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               fz_max2(fz8_lds_fwd(128, 5), (4 * 6 + 8) * FZ_C * (int)sizeof(float))));
-    HIPCHK(hipFuncSetAttribute((const void*)se_bwd8<PREC_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               fz8_lds_bwd(128)));
     for (const void* fn : {(const void*)lz_se_fwd<PREC_F32>, (const void*)lz_se_fwd<PREC_BF16>,
                            (const void*)lz_se_bwd<PREC_F32>, (const void*)lz_se_bwd<PREC_BF16>,
                            (const void*)lz_dec_fwd<PREC_F32>, (const void*)lz_dec_fwd<PREC_BF16>,
@@ -1164,18 +1155,6 @@ static int fused_shape(avc_ctx* ctx, int T) {
     return nf <= 1 ? 1 : nf <= 2 ? 2 : nf <= 4 ? 4 : 8;
 }
 
-// AVC_FZ8=1: bf16 passes of the standard shape on the 8-wave kernels (two waves per SIMD, bitwise
-// the 4-wave results).  Opt-in: measured slower than the 4-wave engine
-static void use_fz8(Launch& L) {
-    if ((L.kind != L_FZ_FWD && L.kind != L_FZ_BWD) || L.prec != PREC_BF16 || L.fz_shape != 0 || L.fz.T != 128) return;
-    const char* e = getenv("AVC_FZ8");
-    if (!(e && e[0] == '1')) return;
-    L.fz8 = true;
-    L.block = dim3(512);
-    L.shmem = std::max(L.shmem, (size_t)(L.kind == L_FZ_FWD ? fz8_lds_fwd(128, 5) : fz8_lds_bwd(128)));
-    L.name = L.kind == L_FZ_FWD ? "se_fwd8<bf16>" : "se_bwd8<bf16>";
-}
-
 static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float* x, bool attack, int prec) {
     const avc_se_cfg& c = ctx->cfg;
     const int B = ws.B;
@@ -1244,11 +1223,9 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
         F.fz.loss_cur = ws.loss_cur.p;
         F.flop += L.flop;
         F.name = "se_fwd_fused<bf16>";
-        use_fz8(F);
         pl.launches.push_back(F);
         return 0;
     }
-    use_fz8(F);
     pl.launches.push_back(F);
     pl.launches.push_back(L);
     return 0;
@@ -1279,7 +1256,6 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
     L.flop = fz_fwd_flop(ctx->cfg, ws.Tl, ctx->bank_k) * ws.B;   // input-gradient only
     L.name = prec == PREC_F32 ? "se_bwd_fused<f32>" : "se_bwd_fused<bf16>";
     if (ws.lz) L.name = prec == PREC_F32 ? "lz_se_bwd<f32>" : "lz_se_bwd<bf16>";
-    use_fz8(L);
     pl.launches.push_back(L);
     return 0;
 }
@@ -1319,10 +1295,11 @@ static bool want_fused(avc_ctx* ctx, int T) { return engine_for(ctx, T) != AVC_E
 
 // long-engine scratch for B utterances of up to T frames and `nlayers` masked layers
 static int alloc_long(LongArgs& L, int B, int T, int nlayers) {
-    // a stride-2 chunk stages 2 * 127 + k + 2 input rows from row LZ_ZR - k/2 whatever the length,
-    // so a short utterance's image must still span them (T <= 178 read past the last image's end:
-    // an illegal address when that end was the end of a mapping)
-    const int rows = std::max(T, 2 * 128) + 2 * LZ_ZR + 64;
+    // pad rows around the frames, + LZ_ZR for the decoder's out_conv^T dY image (zeroed over
+    // Tn + 3 LZ_ZR rows).  Every stage of a chunk window is clipped to these rows in the kernels
+    // (avc_long.hip LzPipe::rows / lz_stage_cap): a stride-2 window spans 2 * 127 + k + 2 rows whatever
+    // the layer's length, which read past a short utterance's image (round 3: T <= 178)
+    const int rows = T + 3 * LZ_ZR + 16;
     L.img_stride = (int64_t)rows * 128 * 4;                 // fp32-sized rows serve both precisions
     L.fl_stride = (int64_t)((T + 32 + 15) / 16 + LZ_FL_EXTRA) * 4 * 2 * 64 * 4;
     L.nFmax = (T + 15) / 16;
@@ -1576,11 +1553,6 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
                       : L.fz_shape == 4 ? AVC_FZ_K(4)
                                         : AVC_FZ_K(8);
 #undef AVC_FZ_K
-        if (L.fz8) {
-            if (L.kind == L_FZ_FWD) klaunch(ev, false, se_fwd8<PREC_BF16>, L.grid, L.block, L.shmem, s, L.fz);
-            else klaunch(ev, false, se_bwd8<PREC_BF16>, L.grid, L.block, L.shmem, s, L.fz);
-            return hipGetLastError();
-        }
         klaunch(ev, false, k, L.grid, L.block, L.shmem, s, L.fz);
         return hipGetLastError();
     }

@@ -19,18 +19,6 @@ __host__ __device__ constexpr int fz_lds_bwd_main(int prec, int T) {
 // + per-wave fold scratch [5*16 ch][8 edge columns] fp32
 __host__ __device__ constexpr int fz_lds_bwd(int prec, int T) { return fz_lds_bwd_main(prec, T) + 4 * 5 * 16 * 8 * 4; }
 
-// the 8-wave bf16 engine at T = 128 (avc_fused8.hip).  Forward: the 4-wave layout + the last block's
-// pool hand-off (4 waves x 2 tiles x 64 lanes x 16 B) after the two block images.  Backward: GB
-// (dY / g_pre0) + GB2, which becomes the two halves' g(b_k) images, + per-wave fold scratch + the
-// last block's pool-adjoint hand-off.
-constexpr int FZ8_XCH = 4 * 2 * 64 * 16;
-__host__ __device__ constexpr int fz8_lds_fwd(int T, int ks) {
-    return fz_max2(fz_lds_fwd(PREC_BF16, T, ks), 2 * (T + 2 * (ks / 2)) * 288 + FZ8_XCH);
-}
-__host__ __device__ constexpr int fz8_lds_bwd(int T) {
-    return fz_max2((T + 8) * 288 + 2 * (T + 16) * 288, 2 * FZ_CIN * (T + 4) * 4) + 8 * 5 * 16 * 8 * 4 + FZ8_XCH;
-}
-
 // fused Decoder (avc_vc.hip) at output length Tn: forward = block-input image + conv1
 // output image, (Tn + 2P) rows each; backward = two dY images (Tn + 8 rows) + per-wave
 // fold scratch [2*16 ch][8 edge columns] fp32.  (+ 32 B static LDS in the forward)

@@ -106,6 +106,15 @@ __device__ __forceinline__ void lz_stage(char* lds, const char* img, int r0, int
     }
 }
 
+// rows of one operand image of this workspace (fp32-sized rows serve both precisions)
+template <int PREC>
+__device__ __forceinline__ int lz_img_rows(const LongArgs& L) { return (int)(L.img_stride / Lz<PREC>::GRB); }
+// lz_stage of rows [r0, r0 + n) clipped to the image's allocated rows (see LzPipe::rows)
+template <int PREC>
+__device__ __forceinline__ void lz_stage_cap(char* lds, const char* img, int r0, int n, const LongArgs& L) {
+    lz_stage<PREC>(lds, img, r0, min(n, lz_img_rows<PREC>(L) - r0));
+}
+
 // rows [r0, r0 + n) of a global operand image -> LDS rows [0, n) (stride RS) by LDS-DMA
 // (global_load_lds_dwordx4), NOT waited for: every wave issues NI 1-KB pieces of the padded
 // LDS layout (a piece's lanes that fall on a row's pad slots or past row n load a duplicate
@@ -148,7 +157,11 @@ struct LzPipe {
     int boff;                                                // second buffer at b0 + boff (0: one buffer)
     bool dma;
     int nfrag;
-    __device__ __forceinline__ LzPipe(char* WB, int nfrag_, int nr_bound) : nfrag(nfrag_) {
+    int cap;                                                 // rows of an operand image (LongArgs::img_stride)
+    // rows [r0, r0 + n) of the window, never past the image's last allocated row (a window is sized
+    // for the longest layer; the rows past a short layer's extent are never read by an owned column)
+    __device__ __forceinline__ int rows(int r0, int n) const { return min(n, cap - r0); }
+    __device__ __forceinline__ LzPipe(char* WB, int nfrag_, int nr_bound, int cap_) : nfrag(nfrag_), cap(cap_) {
         dma = PREC == PREC_BF16 && nr_bound <= NRMAX;
         b0 = WB;
         boff = dma ? LzDma<PREC, NRMAX>::BUFB : 0;
@@ -159,7 +172,7 @@ struct LzPipe {
         LzChunk c0;
         lz_chunk(0, nfrag, LZ_CHF, c0);
         __syncthreads();                                     // earlier readers of b0 are done
-        lz_stage_dma<PREC, NRMAX>(b0, img, r0f(c0), nrf(c0));
+        lz_stage_dma<PREC, NRMAX>(b0, img, r0f(c0), rows(r0f(c0), nrf(c0)));
     }
     // the staged rows of chunk k (all waves may read them on return)
     template <class R0F, class NRF>
@@ -171,7 +184,7 @@ struct LzPipe {
             return b0 + (k & 1) * boff;
         }
         __syncthreads();
-        lz_stage<PREC>(b0, img, r0f(chk), nrf(chk));
+        lz_stage<PREC>(b0, img, r0f(chk), rows(r0f(chk), nrf(chk)));
         __syncthreads();
         return b0;
     }
@@ -180,7 +193,8 @@ struct LzPipe {
     __device__ __forceinline__ void issue_next(int k, const char* img, R0F r0f, NRF nrf) {
         if (!dma) return;
         LzChunk nx;
-        if (lz_chunk(k + 1, nfrag, LZ_CHF, nx)) lz_stage_dma<PREC, NRMAX>(b0 + ((k + 1) & 1) * boff, img, r0f(nx), nrf(nx));
+        if (lz_chunk(k + 1, nfrag, LZ_CHF, nx))
+            lz_stage_dma<PREC, NRMAX>(b0 + ((k + 1) & 1) * boff, img, r0f(nx), rows(r0f(nx), nrf(nx)));
     }
 };
 
@@ -598,7 +612,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         const int nfi = lz_nf(Ti);
         auto r0_c1 = [=](const LzChunk& ch) __attribute__((always_inline)) { return LZ_ZR + 16 * ch.f0 - P; };
         auto nr_c1 = [=](const LzChunk&) __attribute__((always_inline)) { return 127 + ks + 2; };
-        LzPipe<PREC, 136> pipe1(WB, nfi, 127 + ks + 2);
+        LzPipe<PREC, 136> pipe1(WB, nfi, 127 + ks + 2, lz_img_rows<PREC>(L));
         pipe1.prime(imgh, r0_c1, nr_c1);
         for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
@@ -654,7 +668,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         };
         auto r0_c2 = [=](const LzChunk& ch) __attribute__((always_inline)) { return LZ_ZR + s * 16 * ch.f0 - P; };
         auto nr_c2 = [=](const LzChunk&) __attribute__((always_inline)) { return s * 127 + ks + 2; };
-        LzPipe<PREC, 264> pipe2(WB, nfo, s * 127 + ks + 2);
+        LzPipe<PREC, 264> pipe2(WB, nfo, s * 127 + ks + 2, lz_img_rows<PREC>(L));
         pipe2.prime(imgy, r0_c2, nr_c2);
         for (int k = 0; lz_chunk(k, nfo, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
@@ -743,7 +757,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
         for (int k = 0; lz_chunk(k, nfn, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
             __syncthreads();
-            lz_stage<PREC>(WB, imgh, LZ_ZR + n0, 129);
+            lz_stage_cap<PREC>(WB, imgh, LZ_ZR + n0, 129, L);
             __syncthreads();
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, TN - 1) - n0;
@@ -878,7 +892,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         auto nr_g = [=](const LzChunk& ch) __attribute__((always_inline)) {
             return min(16 * ch.f0 + 111, Ti + P - 1) - max(16 * ch.f0 - 16, -P) + ks + 2;
         };
-        LzPipe<PREC, 136> pipeg(WB, nfc, 127 + ks + 2);
+        LzPipe<PREC, 136> pipeg(WB, nfc, 127 + ks + 2, lz_img_rows<PREC>(L));
         pipeg.prime(imgg, r0_g, nr_g);
         for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
@@ -927,7 +941,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         char* nimg = l > 0 ? imgg : imgp;
         float* gprev = gh[cur];
         float* gnew = gh[cur ^ 1];
-        LzPipe<PREC, 136> pipeg2(WB, nfc, 127 + ks + 2);
+        LzPipe<PREC, 136> pipeg2(WB, nfc, 127 + ks + 2, lz_img_rows<PREC>(L));
         pipeg2.prime(imgg2, r0_g, nr_g);
         for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
@@ -1043,7 +1057,7 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
         const int n0 = 16 * chk.f0;
         const int W0 = n0 - 16;                         // first frame of the g(b_k) window
         __syncthreads();
-        lz_stage<PREC>(GP, imgp, LZ_ZR + W0, NFW * 16);
+        lz_stage_cap<PREC>(GP, imgp, LZ_ZR + W0, NFW * 16, L);
         {   // this wave's slice of the GBK margins: zero
             constexpr int V16 = 32 * ESZ / 16;
             for (int idx = lane; idx < 2 * ZPB * V16; idx += 64) {
@@ -1276,7 +1290,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         for (int k = 0; lz_chunk(k, lz_nf(T0), NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
             __syncthreads();
-            lz_stage<PREC>(WB, imgy, LZ_ZR + n0, 129);
+            lz_stage_cap<PREC>(WB, imgy, LZ_ZR + n0, 129, L);
             __syncthreads();
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, T0 - 1) - n0;
@@ -1358,7 +1372,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         // chunk windows staged by LDS-DMA one chunk ahead (LzPipe, as the SpeakerEncoder blocks)
         auto r0_w = [=](const LzChunk& ch) __attribute__((always_inline)) { return LZ_ZR + 16 * ch.f0 - P; };
         auto nr_w = [=](const LzChunk&) __attribute__((always_inline)) { return 127 + ks + 2; };
-        LzPipe<PREC, 136> pipe1(WB, nfi, 127 + ks + 2);
+        LzPipe<PREC, 136> pipe1(WB, nfi, 127 + ks + 2, lz_img_rows<PREC>(L));
         pipe1.prime(imgh, r0_w, nr_w);
         for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
@@ -1393,7 +1407,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         lz_publish();
         // conv2 (up = 1: one GEMM; up = 2: the even / odd half-GEMMs) -> raw over To frames
         const AOp nxt = l + 1 < nblk ? op_c1(l + 1) : op_out();
-        LzPipe<PREC, 136> pipe2(WB, nfi, 127 + ks + 2);
+        LzPipe<PREC, 136> pipe2(WB, nfi, 127 + ks + 2, lz_img_rows<PREC>(L));
         pipe2.prime(imgy, r0_w, nr_w);
         for (int k = 0; lz_chunk(k, nfi, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
@@ -1448,7 +1462,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
     for (int k = 0; lz_chunk(k, lz_nf(Tn), NF, chk); ++k) {
         const int n0 = 16 * chk.f0;
         __syncthreads();
-        lz_stage<PREC>(WB, imgh, LZ_ZR + n0, 129);
+        lz_stage_cap<PREC>(WB, imgh, LZ_ZR + n0, 129, L);
         __syncthreads();
 #pragma unroll
         for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Tn - 1) - n0;
@@ -1574,7 +1588,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
         for (int k = 0; lz_chunk(k, lz_nf(Tn), NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
             __syncthreads();
-            lz_stage<PREC>(WB, imgg, LZ_ZR + n0, 130);
+            lz_stage_cap<PREC>(WB, imgg, LZ_ZR + n0, 130, L);
             __syncthreads();
 #pragma unroll
             for (int f = 0; f < NF; ++f) rb[f] = min(n0 + 16 * f + c, Tn - 1) - n0;
@@ -1718,7 +1732,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
             zero_acc(acc);
             for (int s = 0; s < up; ++s) {
                 __syncthreads();
-                lz_stage<PREC>(WB, s ? imgg2 : imgg, r0, vhi - vlo + ks + 2);
+                lz_stage_cap<PREC>(WB, s ? imgg2 : imgg, r0, vhi - vlo + ks + 2, L);
                 __syncthreads();
                 const AOp nx = s + 1 < up ? op_c2T(l, 1) : (chk.last ? (l > 0 ? op_c1T(l) : op_c2T(l, 0)) : op_c2T(l, 0));
                 fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c2T(l, s), nx, WB, rb);
@@ -1754,7 +1768,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
         auto nr_g = [=](const LzChunk& ch) __attribute__((always_inline)) {
             return min(16 * ch.f0 + 111, Ti + P - 1) - max(16 * ch.f0 - 16, -P) + ks + 2;
         };
-        LzPipe<PREC, 136> pipeg(WB, nfc, 127 + ks + 2);
+        LzPipe<PREC, 136> pipeg(WB, nfc, 127 + ks + 2, lz_img_rows<PREC>(L));
         pipeg.prime(imgg, r0_g, nr_g);
         for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;

@@ -1,5 +1,5 @@
-// The embedding head shared by the 4-wave (avc_fused.hip) and 8-wave (avc_fused8.hip) fused
-// SpeakerEncoder kernels: the standard shape's compile-time constants and the in-kernel head chain
+// The embedding head of the fused SpeakerEncoder kernels (avc_fused.hip): the standard shape's
+// compile-time constants and the in-kernel head chain
 // (time-mean -> dense blocks -> output Linear -> loss -> backward); see avc_fused.hip.
 #pragma once
 #include "avc_fused_core.h"

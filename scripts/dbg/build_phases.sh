@@ -1,10 +1,10 @@
 #!/bin/bash
-# libavc variant with per-phase cycle stamps (-DAVC_FZ_PHASES) in scripts/dbg/ph/
+# libavc variant with per-phase cycle stamps (-DAVC_FZ_PHASES) in scripts/dbg/${PHDIR:-ph}/
+#   EXTRA="-DAVC_FZ_ABLATE=1" PHDIR=ph_a1 scripts/dbg/build_phases.sh
 set -e
 cd "$(dirname "$0")/../.."
-C=attack-vc_amd/csrc; D=scripts/dbg/ph; mkdir -p $D
+C=attack-vc_amd/csrc; D=scripts/dbg/${PHDIR:-ph}; mkdir -p $D
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm --amdgpu-mfma-vgpr-form -mllvm -amdgpu-sched-strategy=max-ilp -DAVC_FZ_PHASES ${EXTRA:-} -c $C/avc_fused.hip -o $D/avc_fused.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm --amdgpu-mfma-vgpr-form -mllvm -amdgpu-sched-strategy=max-ilp -DAVC_FZ_PHASES ${EXTRA:-} -c $C/avc_fused8.hip -o $D/avc_fused8.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $D/libavc.so $C/avc_gemm.hip.o $D/avc_fused.o $D/avc_fused8.o $C/avc_vc.hip.o $C/avc_long.hip.o $C/avc_pm.hip.o $C/avc_dsp.hip.o $C/avc_api.hip.o $C/avc_kernels.hip.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $D/libavc.so $C/avc_gemm.hip.o $D/avc_fused.o $C/avc_vc.hip.o $C/avc_long.hip.o $C/avc_pm.hip.o $C/avc_dsp.hip.o $C/avc_api.hip.o $C/avc_kernels.hip.o
 /opt/rocm/bin/hipcc -O2 -std=c++17 -o $D/avc_bench $C/avc_bench_main.cpp -L$D -lavc -Wl,-rpath,'$ORIGIN'
-rm $D/avc_fused.o $D/avc_fused8.o
+rm $D/avc_fused.o

@@ -4,6 +4,6 @@ set -e
 cd "$(dirname "$0")/../.."
 C=attack-vc_amd/csrc; D=scripts/dbg/phl; mkdir -p $D
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm --amdgpu-mfma-vgpr-form -mllvm -amdgpu-sched-strategy=max-ilp -DAVC_FZ_PHASES -DFZ_PH_MAX=320 ${EXTRA:-} -c $C/avc_long.hip -o $D/avc_long.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $D/libavc.so $C/avc_gemm.hip.o $C/avc_fused.hip.o $C/avc_fused8.hip.o $C/avc_vc.hip.o $D/avc_long.o $C/avc_pm.hip.o $C/avc_dsp.hip.o $C/avc_api.hip.o $C/avc_kernels.hip.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $D/libavc.so $C/avc_gemm.hip.o $C/avc_fused.hip.o $C/avc_vc.hip.o $D/avc_long.o $C/avc_pm.hip.o $C/avc_dsp.hip.o $C/avc_api.hip.o $C/avc_kernels.hip.o
 /opt/rocm/bin/hipcc -O2 -std=c++17 -o $D/avc_bench $C/avc_bench_main.cpp -L$D -lavc -Wl,-rpath,'$ORIGIN'
 rm $D/avc_long.o

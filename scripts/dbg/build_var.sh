@@ -9,7 +9,7 @@ SRCS=${@:-avc_fused.hip}
 D=scripts/dbg/var/$N; mkdir -p $D
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Wno-unused-value -mllvm --amdgpu-mfma-vgpr-form ${SCHED--mllvm -amdgpu-sched-strategy=max-ilp} -DAVC_SRC_HASH=\"var-$N\""
 OBJS=""
-for s in avc_gemm avc_kernels avc_fused avc_fused8 avc_vc avc_long avc_pm avc_dsp avc_api; do
+for s in avc_gemm avc_kernels avc_fused avc_vc avc_long avc_pm avc_dsp avc_api; do
   if [[ " $SRCS " == *" $s.hip "* ]]; then
     /opt/rocm/bin/hipcc $FL $X -c $C/$s.hip -o $D/$s.o
     OBJS="$OBJS $D/$s.o"
