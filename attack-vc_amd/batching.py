@@ -117,7 +117,10 @@ def attack_many(kind: str, model_per_device: Sequence[torch.nn.Module], vc_tgts:
                 # the cache holds them all, so a repeated call over the same lengths re-plans nothing
                 shapes = {(len(g), adv_tgts[need[d][g[0]]].shape[1]) for g in adv_groups}
                 shapes |= {(len(chunks[j]), keys[chunks[j][0]][0]) for j in owner[d]}
-                ctx.set_ws_cache(min(64, max(6, len(shapes) + 2)))
+                # e2e / fb: the ContentEncoder / Decoder workspaces are keyed by (B, T, T_src) and share
+                # the cap with the SpeakerEncoder ones
+                vc_shapes = {(len(chunks[j]),) + tuple(keys[chunks[j][0]]) for j in owner[d]} if kind != "emb" else set()
+                ctx.set_ws_cache(min(64, max(6, max(len(shapes), len(vc_shapes)) + 2)))
                 emb: Dict[int, torch.Tensor] = {}
                 for g in adv_groups:
                     ids = [need[d][k] for k in g]

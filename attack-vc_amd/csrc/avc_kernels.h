@@ -263,6 +263,7 @@ struct DenseArgs {
     const float* bias;                // [M] or null (added by slice 0 only)
     float* Y;                         // [gridDim.z][B][M]
     int32_t M, K, B, kchunk;
+    int32_t nj;                       // dense_mfma: 16-utterance tiles per wave (2 or 4; grid.y = B / 16 nj)
 };
 
 // VSMask PredictiveModel layer (avc_pm.hip): implicit GEMM over NCHW activations.

@@ -805,13 +805,17 @@ __global__ void __launch_bounds__(256) dense_batched(DenseArgs D) {
 // output sums its k in one fixed order that does not depend on the batch (shard invariance).
 // Needs K and kchunk multiples of 4 (16-byte loads); the host falls back to dense_batched.
 // The VALU kernel above ran 13.7 us per conv_affine call at B = 256 (latency / issue bound).
+// NJ 16-utterance tiles per wave (a workgroup: 64 rows x 16 NJ utterances); every output's MFMA
+// sequence over k is the same for any NJ (and any batch), so the results are bitwise NJ-invariant
+template <int NJ>
 __global__ void __launch_bounds__(256) dense_mfma(DenseArgs D) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r16 = l & 15, kq = l >> 4;
-    const int m0 = blockIdx.x * 64 + 16 * w, b0 = blockIdx.y * 32;
+    const int m0 = blockIdx.x * 64 + 16 * w, b0 = blockIdx.y * 16 * NJ;
     const int kb = blockIdx.z * D.kchunk, ke = min(D.K, kb + D.kchunk);
     const float* Ar = D.A + (size_t)min(m0 + r16, D.M - 1) * D.K;       // rows / utterances past
-    const float* X0 = D.X + (size_t)min(b0 + r16, D.B - 1) * D.K;       // the end read a valid
-    const float* X1 = D.X + (size_t)min(b0 + 16 + r16, D.B - 1) * D.K;  // row; never stored
+    const float* Xr[NJ];                                                 // the end read a valid
+#pragma unroll                                                           // row; never stored
+    for (int j = 0; j < NJ; ++j) Xr[j] = D.X + (size_t)min(b0 + 16 * j + r16, D.B - 1) * D.K;
     auto ld = [&](const float* row, int k) __attribute__((always_inline)) {
         if (k + 4 <= ke) return *reinterpret_cast<const f32x4*>(row + k);
         f32x4 v;
@@ -820,33 +824,34 @@ __global__ void __launch_bounds__(256) dense_mfma(DenseArgs D) {
         return v;
     };
     constexpr int U = 4;                        // 16-k steps per chunk; the next chunk is in flight
-    f32x4 ca[U], c0[U], c1[U], na[U], n0[U], n1[U];
-    auto load = [&](int s0, f32x4 (&a)[U], f32x4 (&x0)[U], f32x4 (&x1)[U]) __attribute__((always_inline)) {
+    f32x4 ca[U], cx[NJ][U], na[U], nx[NJ][U];
+    auto load = [&](int s0, f32x4 (&a)[U], f32x4 (&x)[NJ][U]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int k = kb + 16 * (s0 + u) + 4 * kq;
             a[u] = ld(Ar, k);
-            x0[u] = ld(X0, k);
-            x1[u] = ld(X1, k);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) x[j][u] = ld(Xr[j], k);
         }
     };
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int ns = (ke - kb + 15) / 16;
-    load(0, ca, c0, c1);
+    load(0, ca, cx);
     for (int s = 0; s < ns; s += U) {
-        if (s + U < ns) load(s + U, na, n0, n1);
+        if (s + U < ns) load(s + U, na, nx);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][e], c0[u][e], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][e], c1[u][e], acc1, 0, 0, 0);
-            }
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[u][e], cx[j][u][e], acc[j], 0, 0, 0);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             ca[u] = na[u];
-            c0[u] = n0[u];
-            c1[u] = n1[u];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) cx[j][u] = nx[j][u];
         }
     }
     // C layout: lane (r, q) holds utterance b0 + 16j + r, rows m0 + 4q + 0..3
@@ -857,10 +862,10 @@ __global__ void __launch_bounds__(256) dense_mfma(DenseArgs D) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) bi[r] = m + r < D.M ? D.bias[m + r] : 0.f;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
         const int bb = b0 + 16 * j + r16;
         if (bb >= D.B) continue;
-        const f32x4 y = (j ? acc1 : acc0) + bi;
+        const f32x4 y = acc[j] + bi;
         if ((D.M & 3) == 0 && m + 3 < D.M) {   // 4 consecutive rows: one 16-byte store
             *reinterpret_cast<f32x4*>(Y + (size_t)bb * D.M + m) = y;
         } else {
@@ -870,6 +875,8 @@ __global__ void __launch_bounds__(256) dense_mfma(DenseArgs D) {
         }
     }
 }
+template __global__ void dense_mfma<2>(DenseArgs);
+template __global__ void dense_mfma<4>(DenseArgs);
 
 #define AVC_DZ_INST(P, S)                                          \
     template __global__ void dec_fwd_fused<P, S>(DecArgs);        \

@@ -62,6 +62,8 @@ class UniversalPerturbationHeader:
         g = optimizer.param_groups[0]
         if g.get("amsgrad") or g.get("weight_decay", 0) or g.get("maximize"):
             raise RuntimeError("libavc implements plain Adam (no amsgrad / weight_decay / maximize)")
+        if g.get("differentiable"):
+            raise RuntimeError("libavc's header optimiser does not record an autograd graph (differentiable=True)")
         ctx = avc_native.context_for(speaker_encoder, src.device)
         hdr0 = self.header.detach()[0, 0]
         # torch Adam's per-parameter state for the header (created on its first step)
@@ -80,8 +82,12 @@ class UniversalPerturbationHeader:
             self.header.data.copy_(new.reshape(self.header.shape))
         if int(num_iterations) > 0:
             shape = self.header.shape
+            # torch keeps `step` as a float32 scalar tensor, on the parameter's device when the
+            # optimizer is capturable / fused (torch.optim.adam's _get_scalar_dtype / device rule)
+            on_dev = bool(g.get("capturable") or g.get("fused"))
             optimizer.state[self.header] = {
-                "step": torch.tensor(float(step0 + int(num_iterations))),
+                "step": torch.tensor(float(step0 + int(num_iterations)), dtype=torch.float32,
+                                     device=self.header.device if on_dev else "cpu"),
                 "exp_avg": m.reshape(shape).to(self.header.dtype),
                 "exp_avg_sq": v.reshape(shape).to(self.header.dtype)}
         batch = losses.mean(dim=1).cpu()

@@ -168,7 +168,10 @@ int avc_content_encoder(avc_ctx* ctx, const float* x, int B, int T, float* mu, f
 int avc_content_frames(avc_ctx* ctx, int T);
 
 /* Decoder.forward (models.py:403-435): out [B, c_out, Tz * prod(upsample)] = Decoder(z [B, c_in, Tz],
- * cond [B, c_cond]).  fp32. */
+ * cond [B, c_cond]).  fp32.  Runs on the VC attack workspace of the shape (B, Tz * prod(subsample)):
+ * the first call at a new Tz builds it (buffers, plans, autotune -- a SpeakerEncoder workspace included,
+ * cached like an attack's, avc_set_ws_cache), and it needs the fused or long engine (it fails under
+ * AVC_ENGINE_LAYERED, like the e2e / fb attacks). */
 int avc_decoder(avc_ctx* ctx, const float* z, int B, int Tz, const float* cond, float* out, void* stream);
 
 /* End-to-end attack (attack_utils.py:7-48) and feedback attack (attack_utils.py:89-130):
@@ -334,6 +337,7 @@ int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len, long* laun
  *   builds   workspaces allocated and planned for a new shape
  *   replans  a cached workspace re-planned because a call needed more iterations than it holds
  *   hits     calls served by a cached workspace as it was
+ *   (the e2e / fb ContentEncoder / Decoder workspaces, keyed by (B, T, T_src), count in the same totals)
  *   captures hipGraphs captured (attack loops, header optimiser)
  *   evictions cached workspaces freed to make room */
 int avc_ws_stats(avc_ctx* ctx, int64_t* builds, int64_t* replans, int64_t* hits, int64_t* captures,

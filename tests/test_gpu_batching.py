@@ -77,10 +77,23 @@ def test_attack_many_bf16_two_devices_listed(full):
 
 @pytest.mark.parametrize("kind", ["e2e", "fb"])
 def test_attack_many_vc_equals_per_utterance(full, kind):
-    """e2e / fb: buckets keyed by (vc_tgt length, vc_src length); adv_tgt at its own length."""
+    """e2e / fb: buckets keyed by (vc_tgt length, vc_src length); adv_tgt at its own length.  A second
+    call over the same lengths re-plans nothing: the cache is sized for the SpeakerEncoder shapes AND
+    the ContentEncoder / Decoder workspaces keyed by (B, T, T_src)."""
     m = full
+    ctx = avc_native.vc_context_for(m, DEV)
     vc, at, p0, src = _utts(6, [128, 96, 160], [128, 100], seed=5, src_lengths=[128, 72])
     out = batching.attack_many(kind, [m], vc, at, 0.1, 3, vc_srcs=src, ptb0s=p0)
+    torch.cuda.synchronize()
+    s1 = ctx.ws_stats()
+    again = batching.attack_many(kind, [m], vc, at, 0.1, 3, vc_srcs=src, ptb0s=p0)
+    torch.cuda.synchronize()
+    s2 = ctx.ws_stats()
+    for k in ("builds", "replans", "captures", "evictions"):
+        assert s2[k] == s1[k], (k, s1, s2)
+    assert s2["hits"] > s1["hits"]
+    for a, b in zip(out, again):
+        assert torch.equal(a, b)
     fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
     for i in range(6):
         ref = fn(m, src[i][None], vc[i][None], at[i][None], 0.1, 3, ptb0=p0[i][None]).detach()[0]
