@@ -47,6 +47,7 @@ __global__ void dec_bwd_fused(DecArgs A);
 __global__ void dense_batched(DenseArgs D);
 template <int NJ>
 __global__ void dense_mfma(DenseArgs D);
+__global__ void dense_lds(DenseArgs D);
 __global__ void hdr_compose(HdrArgs A);
 __global__ void hdr_update(HdrArgs A);
 __global__ void pm_conv(PmConvArgs P);
@@ -1571,10 +1572,11 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
     case L_DENSE:
         // fp32 MFMA tiles when the rows take 16-byte loads (K, kchunk multiples of 4; always on
         // the AdaIN-VC config), the VALU kernel otherwise
-        if (L.dn.K % 4 == 0 && L.dn.kchunk % 4 == 0) {
-            if (L.dn.nj == 4) klaunch(ev, false, dense_mfma<4>, L.grid, L.block, 0, s, L.dn);
-            else klaunch(ev, false, dense_mfma<2>, L.grid, L.block, 0, s, L.dn);
-        } else
+        if (L.dn.variant == DZ_LDS)
+            klaunch(ev, false, dense_lds, L.grid, L.block, L.shmem, s, L.dn);
+        else if (L.dn.variant == DZ_MFMA)
+            klaunch(ev, false, dense_mfma<2>, L.grid, L.block, 0, s, L.dn);
+        else
             klaunch(ev, false, dense_batched, L.grid, L.block, 0, s, L.dn);
         return hipGetLastError();
     case L_HDR_COMPOSE:

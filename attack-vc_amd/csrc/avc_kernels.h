@@ -257,13 +257,14 @@ struct DecArgs {
 // (the decoder's conv_affine Linear layers and their transposes).
 // Split-K (gridDim.z = K / kchunk slices): slice z sums k in [z*kchunk, (z+1)*kchunk) into
 // Y + z*B*M; the consumer adds the slices in a fixed order (deterministic, no atomics).
+enum { DZ_VALU = 0, DZ_MFMA = 1, DZ_LDS = 2 };
 struct DenseArgs {
     const float* A;                   // [M][K] row-major
     const float* X;                   // [B][K]
     const float* bias;                // [M] or null (added by slice 0 only)
     float* Y;                         // [gridDim.z][B][M]
     int32_t M, K, B, kchunk;
-    int32_t nj;                       // dense_mfma: 16-utterance tiles per wave (2 or 4; grid.y = B / 16 nj)
+    int32_t variant;                  // DZ_VALU / DZ_MFMA / DZ_LDS (host-chosen; fixes the grid)
 };
 
 // VSMask PredictiveModel layer (avc_pm.hip): implicit GEMM over NCHW activations.

@@ -876,7 +876,68 @@ __global__ void __launch_bounds__(256) dense_mfma(DenseArgs D) {
     }
 }
 template __global__ void dense_mfma<2>(DenseArgs);
-template __global__ void dense_mfma<4>(DenseArgs);
+
+// The same MFMA sequence with both operand tiles staged through LDS first (the default when a K
+// slice is at most DZ_KC wide: conv_affine's K = 128, conv_affine^T's 128-wide slices).  In
+// dense_mfma every wave loads its own rows and ALL the tile's utterances with 16-byte loads that
+// touch 16 rows at a time -- 40 scattered loads per lane, ~4.6 of its ~9 us (scripts/dbg/
+// densebench.hip).  Here the workgroup's 256 threads read the [64 rows][kc] A tile and the
+// [16][kc] X tile once, with contiguous 16-byte loads all in flight together, write them to LDS
+// (row stride DZ_KC + 4 floats: a 16-lane fragment read covers the 64 banks once) and run the
+// K loop from ds_read_b128 fragments in dense_mfma's order: bitwise the same outputs (the
+// microbenchmark compares all 786k), 4.9 instead of 8.8 us per conv_affine call.
+constexpr int DZ_KC = 128, DZ_KS = DZ_KC + 4;
+__global__ void __launch_bounds__(256) dense_lds(DenseArgs D) {
+    extern __shared__ float lds[];
+    float* As = lds;                      // [64][DZ_KS]
+    float* Xs = lds + 64 * DZ_KS;         // [16][DZ_KS]
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, r16 = l & 15, kq = l >> 4;
+    const int mb = blockIdx.x * 64, b0 = blockIdx.y * 16;
+    const int kb = blockIdx.z * D.kchunk, kc = min(D.K, kb + D.kchunk) - kb;
+    constexpr int RQ = DZ_KC / 4, NA = 64 * RQ, NT = (NA + 16 * RQ) / 256;
+    f32x4 v[NT];
+#pragma unroll
+    for (int r = 0; r < NT; ++r) {        // rows / utterances past the end read a valid row
+        const int i = t + 256 * r;
+        const bool isA = i < NA;
+        const int ii = isA ? i : i - NA, row = ii / RQ, k = 4 * (ii % RQ);
+        const float* src = isA ? D.A + (size_t)min(mb + row, D.M - 1) * D.K : D.X + (size_t)min(b0 + row, D.B - 1) * D.K;
+        v[r] = k < kc ? *reinterpret_cast<const f32x4*>(src + kb + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int r = 0; r < NT; ++r) {
+        const int i = t + 256 * r;
+        const bool isA = i < NA;
+        const int ii = isA ? i : i - NA, row = ii / RQ, k = 4 * (ii % RQ);
+        *reinterpret_cast<f32x4*>((isA ? As : Xs) + row * DZ_KS + k) = v[r];
+    }
+    __syncthreads();
+    const float* ar = As + (16 * w + r16) * DZ_KS + 4 * kq;
+    const float* xr = Xs + r16 * DZ_KS + 4 * kq;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int ns = (kc + 15) / 16;
+    for (int s = 0; s < ns; ++s) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(ar + 16 * s);
+        const f32x4 x = *reinterpret_cast<const f32x4*>(xr + 16 * s);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], x[e], acc, 0, 0, 0);
+    }
+    const int m = mb + 16 * w + 4 * kq, bb = b0 + r16;
+    if (bb >= D.B) return;
+    float* Y = D.Y + (size_t)blockIdx.z * D.B * D.M + (size_t)bb * D.M;
+    f32x4 bi = {0.f, 0.f, 0.f, 0.f};
+    if (D.bias && blockIdx.z == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bi[r] = m + r < D.M ? D.bias[m + r] : 0.f;
+    const f32x4 y = acc + bi;
+    if ((D.M & 3) == 0 && m + 3 < D.M) {
+        *reinterpret_cast<f32x4*>(Y + m) = y;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m + r < D.M) Y[m + r] = y[r];
+    }
+}
 
 #define AVC_DZ_INST(P, S)                                          \
     template __global__ void dec_fwd_fused<P, S>(DecArgs);        \
