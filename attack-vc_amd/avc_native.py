@@ -54,7 +54,8 @@ UPDATE = {"adam": 0, "pgd": 1}
 class DspCfg(ctypes.Structure):
     _fields_ = [("sample_rate", ctypes.c_int32), ("n_fft", ctypes.c_int32), ("hop_length", ctypes.c_int32),
                 ("win_length", ctypes.c_int32), ("n_mels", ctypes.c_int32), ("preemph", ctypes.c_float),
-                ("ref_db", ctypes.c_float), ("max_db", ctypes.c_float), ("pad_mode", ctypes.c_int32)]
+                ("ref_db", ctypes.c_float), ("max_db", ctypes.c_float), ("pad_mode", ctypes.c_int32),
+                ("flavor", ctypes.c_int32)]
 
 
 PAD_MODE = {"reflect": 0, "constant": 1}
@@ -138,6 +139,11 @@ SIGNATURES = [
                                        ctypes.c_void_p]),
     ("avc_dsp_griffin_lim", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_dsp_ta_mel2wav", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("avc_vsmask_band_clamp", ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
     ("avc_dsp_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_dsp_profile_count", ctypes.c_int, [ctypes.c_void_p]),
     ("avc_dsp_profile_kernel", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
@@ -712,6 +718,23 @@ def vsmask_apply_header(mel: torch.Tensor, header: torch.Tensor) -> torch.Tensor
     return out
 
 
+def vsmask_band_clamp(x: torch.Tensor, eps1: float, eps2: float, eps3: float) -> torch.Tensor:
+    """MelSpectrogramConverter.apply_weighted_constraint (utils/audio.py:77-116): x [..., F, T]
+    clamped to +-eps1 / eps2 / eps3 on rows [0, int(0.3 F)) / [.., int(0.7 F)) / the rest."""
+    _require_gpu(x)
+    if x.dim() < 2:
+        raise RuntimeError(f"expected [..., F, T], got {tuple(x.shape)}")
+    xc = x.float().contiguous()
+    F, T = xc.shape[-2], xc.shape[-1]
+    B = xc.numel() // max(F * T, 1)
+    out = torch.empty_like(xc)
+    dev = xc.device.index if xc.device.index is not None else torch.cuda.current_device()
+    _check(lib().avc_vsmask_band_clamp(dev, ctypes.c_void_p(xc.data_ptr()), B, F, T, float(eps1), float(eps2),
+                                       float(eps3), ctypes.c_void_p(out.data_ptr()),
+                                       ctypes.c_void_p(torch.cuda.current_stream(xc.device).cuda_stream)))
+    return out
+
+
 def vsmask_windows(T: int, window_size: int = 100, future_step: int = 10) -> int:
     """Number of predictor windows of the reference loop, len(range(0, T - W, S))."""
     n = ctypes.c_int()
@@ -750,7 +773,8 @@ def pm_context_for(model: torch.nn.Module, device: torch.device) -> "PMContext":
 # --- mel front / back end (data_utils.py:16-197) ------------------------------------
 
 def dsp_cfg_struct(preprocess: Dict, pad_mode: str = "reflect") -> DspCfg:
-    """config.yaml `preprocess` section -> avc_dsp_cfg (top_db is host-side: trim)."""
+    """config.yaml `preprocess` section -> avc_dsp_cfg (top_db is host-side: trim).  A
+    `flavor: 1` entry selects utils/audio.py's torchaudio converter (TA_PREPROCESS below)."""
     c = DspCfg()
     for k in ("sample_rate", "n_fft", "hop_length", "win_length", "n_mels"):
         setattr(c, k, int(preprocess[k]))
@@ -759,7 +783,15 @@ def dsp_cfg_struct(preprocess: Dict, pad_mode: str = "reflect") -> DspCfg:
     if pad_mode not in PAD_MODE:
         raise RuntimeError(f"pad_mode must be one of {sorted(PAD_MODE)}")
     c.pad_mode = PAD_MODE[pad_mode]
+    c.flavor = int(preprocess.get("flavor", 0))
     return c
+
+
+def ta_preprocess(sample_rate: int = 16000, n_fft: int = 1024, hop_length: int = 256, n_mels: int = 80) -> Dict:
+    """utils/audio.py:9-42's MelSpectrogram / InverseMelScale / GriffinLim parameters as an
+    avc_dsp_cfg source (win_length = n_fft, no pre-emphasis, reflect padding, flavor 1)."""
+    return dict(sample_rate=int(sample_rate), n_fft=int(n_fft), hop_length=int(hop_length), win_length=int(n_fft),
+                n_mels=int(n_mels), preemph=0.0, ref_db=0.0, max_db=0.0, flavor=1)
 
 
 def mel_basis(preprocess: Dict):
@@ -858,6 +890,32 @@ class Dsp:
             _check(lib().avc_dsp_griffin_lim(self.h, ctypes.c_void_p(spect.data_ptr()), B, Tf, int(n_iter),
                                              ctypes.c_void_p(out.data_ptr()),
                                              ctypes.c_void_p(torch.cuda.current_stream(spect.device).cuda_stream)))
+        return out
+
+    def ta_mel2wav(self, mel: torch.Tensor, n_iter: int = 32, momentum: float = 0.99,
+                   angles0: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """flavor-1 context: log10 mel [B, n_mels, Tf] -> wav [B, hop * (Tf - 1)] (InverseMelScale +
+        GriffinLim; angles0 [B, n_fft/2+1, Tf] complex64 initial phases or None for all ones)."""
+        _require_gpu(mel)
+        mel = mel.float().contiguous()
+        nm, F = int(self.pre["n_mels"]), int(self.pre["n_fft"]) // 2 + 1
+        if mel.dim() != 3 or mel.shape[1] != nm:
+            raise RuntimeError(f"expected log-mel [B, {nm}, Tf], got {tuple(mel.shape)}")
+        B, _, Tf = mel.shape
+        if angles0 is not None:
+            if angles0.dtype != torch.complex64 or tuple(angles0.shape) != (B, F, Tf):
+                raise RuntimeError(f"angles0 must be complex64 [{B}, {F}, {Tf}], got {angles0.dtype} "
+                                   f"{tuple(angles0.shape)}")
+            if angles0.device != mel.device:
+                raise RuntimeError("angles0 must be on the mel's device")
+            angles0 = angles0.contiguous()
+        out = torch.empty(B, int(self.pre["hop_length"]) * (Tf - 1), device=mel.device)
+        with self._lock:
+            _check(lib().avc_dsp_ta_mel2wav(self.h, ctypes.c_void_p(mel.data_ptr()), B, Tf, int(n_iter),
+                                            float(momentum),
+                                            ctypes.c_void_p(angles0.data_ptr()) if angles0 is not None else None,
+                                            ctypes.c_void_p(out.data_ptr()),
+                                            ctypes.c_void_p(torch.cuda.current_stream(mel.device).cuda_stream)))
         return out
 
     def set_profiling(self, on: bool):

@@ -1,4 +1,5 @@
-// Mel front / back end of the reference (data_utils.py:16-197) on gfx950:
+// Mel front / back end of the reference (data_utils.py:16-197; flavor 1: utils/audio.py:8-76,
+// the torchaudio MelSpectrogram / InverseMelScale / GriffinLim of the VSMask converter) on gfx950:
 //   dsp_wav2mel    file2mel after load + trim (data_utils.py:99-118): pre-emphasis,
 //                  centered STFT, |X|, mel projection, dB, clip (+ normalize, 35-47)
 //   dsp_mel2mag    mel2wav's front (150-157): (denormalize,) clip, dB^-1, inv_mel_matrix
@@ -121,8 +122,9 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
     for (int k = threadIdx.x; k < F; k += DSP_THREADS) {
         float2 X0, X1;
         split_pair(Z, N, k, X0, X1);
-        MAG[k] = sqrtf(X0.x * X0.x + X0.y * X0.y);
-        MAG[F + k] = sqrtf(X1.x * X1.x + X1.y * X1.y);
+        const float p0 = X0.x * X0.x + X0.y * X0.y, p1 = X1.x * X1.x + X1.y * X1.y;
+        MAG[k] = A.flavor ? p0 : sqrtf(p0);            // torchaudio MelSpectrogram: power 2
+        MAG[F + k] = A.flavor ? p1 : sqrtf(p1);
     }
     __syncthreads();
     for (int idx = threadIdx.x; idx < 2 * A.n_mels; idx += DSP_THREADS) {
@@ -132,10 +134,15 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
         const float* mg = MAG + fr * F;
         float s = 0.f;
         for (int f = A.mel_range[2 * m]; f < A.mel_range[2 * m + 1]; ++f) s = fmaf(row[f], mg[f], s);
-        // 20 log10(max(1e-5, mel)); clip((mel - ref_db + max_db) / max_db, 1e-8, 1) (111-112)
-        float v = 20.f * log10f(fmaxf(1e-5f, s));
-        v = fminf(fmaxf((v - A.ref_db + A.max_db) / A.max_db, 1e-8f), 1.f);
-        if (A.mean) v = (v - A.mean[m]) / A.std[m];        // normalize (data_utils.py:35-47)
+        float v;
+        if (A.flavor) {
+            v = log10f(fmaxf(s, 1e-5f));                   // log10(clamp(mel, 1e-5)) (utils/audio.py:55-56)
+        } else {
+            // 20 log10(max(1e-5, mel)); clip((mel - ref_db + max_db) / max_db, 1e-8, 1) (111-112)
+            v = 20.f * log10f(fmaxf(1e-5f, s));
+            v = fminf(fmaxf((v - A.ref_db + A.max_db) / A.max_db, 1e-8f), 1.f);
+            if (A.mean) v = (v - A.mean[m]) / A.std[m];    // normalize (data_utils.py:35-47)
+        }
         const size_t o = A.transpose ? ((size_t)b * A.n_mels + m) * Tf + t : ((size_t)b * Tf + t) * A.n_mels + m;
         A.mel_out[o] = v;
     }
@@ -149,6 +156,10 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_mel2mag(DspArgs A) {
     const int t = blockIdx.x, b = blockIdx.y, nm = A.n_mels, Tf = A.Tf;
     for (int m = threadIdx.x; m < nm; m += DSP_THREADS) {
         float v = A.mel_in[A.transpose ? ((size_t)b * nm + m) * Tf + t : ((size_t)b * Tf + t) * nm + m];
+        if (A.flavor) {                                    // pow(10, mel) (utils/audio.py:70)
+            lin[m] = exp10f(v);
+            continue;
+        }
         if (A.mean) v = v * A.std[m] + A.mean[m];          // denormalize (data_utils.py:50-62)
         v = fminf(fmaxf(v, 0.f), 1.f) * A.max_db - A.max_db + A.ref_db;
         lin[m] = exp10f(v * 0.05f);
@@ -158,7 +169,9 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_mel2mag(DspArgs A) {
         // inv_mel stored transposed [n_mels][F]: consecutive threads read consecutive bins
         float s = 0.f;
         for (int m = 0; m < nm; ++m) s = fmaf(A.inv_mel[(size_t)m * A.F + f], lin[m], s);
-        A.spect_out[((size_t)b * Tf + t) * A.F + f] = s;
+        // flavor 1: InverseMelScale's relu of the least-squares solution, then GriffinLim's
+        // specgram.pow(1 / power) (power 2): the magnitude
+        A.spect_out[((size_t)b * Tf + t) * A.F + f] = A.flavor ? sqrtf(fmaxf(s, 0.f)) : s;
     }
 }
 
@@ -193,11 +206,26 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
         m1[i] = (k < F && has1) ? S1[k] : 0.f;
     }
     float2 X0[KPT], X1[KPT];
+    // flavor 1: the previous rebuilt spectra of the two frames
+    float2* P0 = A.flavor ? reinterpret_cast<float2*>(A.tprev) + ((size_t)b * Tf + t0) * F : nullptr;
+    float2* P1 = A.flavor ? P0 + F : nullptr;
     if (A.init) {
 #pragma unroll
         for (int i = 0; i < KPT; ++i) {
+            const int k = tid + DSP_THREADS * i;
             X0[i] = make_float2(m0[i], 0.f);
             X1[i] = make_float2(m1[i], 0.f);
+            if (A.flavor && k < F) {
+                // X = |S| * angles0 (torch.rand complex: NOT unit modulus); tprev = 0
+                if (A.angles0) {
+                    const float2* a0 = reinterpret_cast<const float2*>(A.angles0) + ((size_t)b * F + k) * Tf;
+                    const float2 u = a0[t0], v = has1 ? a0[t1] : make_float2(0.f, 0.f);
+                    X0[i] = make_float2(m0[i] * u.x, m0[i] * u.y);
+                    X1[i] = make_float2(m1[i] * v.x, m1[i] * v.y);
+                }
+                P0[k] = make_float2(0.f, 0.f);
+                if (has1) P1[k] = make_float2(0.f, 0.f);
+            }
         }
         stage_twiddles(TW, A.twiddle, N);
     } else {
@@ -220,10 +248,25 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
             if (k < F) {
                 float2 E0, E1;
                 split_pair(Z, N, k, E0, E1);
-                const float s0 = m0[i] / fmaxf(1e-8f, sqrtf(E0.x * E0.x + E0.y * E0.y));
-                const float s1 = has1 ? m1[i] / fmaxf(1e-8f, sqrtf(E1.x * E1.x + E1.y * E1.y)) : 0.f;
-                X0[i] = make_float2(E0.x * s0, E0.y * s0);
-                X1[i] = make_float2(E1.x * s1, E1.y * s1);
+                if (A.flavor) {
+                    // torchaudio griffinlim: angles = rebuilt - alpha * tprev; angles /= |angles| +
+                    // 1e-16; tprev = rebuilt; X = |S| * angles
+                    const float al = A.momentum / (1.f + A.momentum);
+                    const float2 q0 = P0[k], q1 = has1 ? P1[k] : make_float2(0.f, 0.f);
+                    const float2 a0 = make_float2(E0.x - al * q0.x, E0.y - al * q0.y);
+                    const float2 a1 = make_float2(E1.x - al * q1.x, E1.y - al * q1.y);
+                    const float s0 = m0[i] / (sqrtf(a0.x * a0.x + a0.y * a0.y) + 1e-16f);
+                    const float s1 = has1 ? m1[i] / (sqrtf(a1.x * a1.x + a1.y * a1.y) + 1e-16f) : 0.f;
+                    X0[i] = make_float2(a0.x * s0, a0.y * s0);
+                    X1[i] = make_float2(a1.x * s1, a1.y * s1);
+                    P0[k] = E0;
+                    if (has1) P1[k] = E1;
+                } else {
+                    const float s0 = m0[i] / fmaxf(1e-8f, sqrtf(E0.x * E0.x + E0.y * E0.y));
+                    const float s1 = has1 ? m1[i] / fmaxf(1e-8f, sqrtf(E1.x * E1.x + E1.y * E1.y)) : 0.f;
+                    X0[i] = make_float2(E0.x * s0, E0.y * s0);
+                    X1[i] = make_float2(E1.x * s1, E1.y * s1);
+                }
             }
         }
     }

@@ -321,7 +321,8 @@ struct VsmArgs {
     int low_end, high_start;          // band edges int(F*0.3), int(F*0.7) (utils/audio.py:97-98)
     float eps1, eps2, eps3;
     int mode;                         // 0 = protect (band clamp of the summed perturbation),
-                                      // 1 = header_model.apply_header (clamp the sum to [-1, 1])
+                                      // 1 = header_model.apply_header (clamp the sum to [-1, 1]),
+                                      // 2 = apply_weighted_constraint alone (band clamp of mel)
 };
 
 // Mel front / back end (avc_dsp.hip; data_utils.py:16-197).  One workgroup per pair of
@@ -350,6 +351,12 @@ struct DspArgs {
     float* frames;                     // [B][Tf][N] windowed inverse-FFT frames
     float* y;                          // [B][Ly] overlap-added signal
     float* wav;                        // [B][Ly] de-emphasised output
+    // flavor 1: utils/audio.py's torchaudio converter (power-2 STFT, log10 mel, pinv inverse,
+    // Griffin-Lim with momentum from given initial angles); 0: data_utils.py's librosa pipeline
+    int32_t flavor;
+    float momentum;                    // flavor 1 Griffin-Lim: alpha = momentum / (1 + momentum)
+    const float* angles0;              // [B][F][Tf] complex64 initial angles (torch layout), or null: 1
+    float* tprev;                      // [B][Tf][F] complex: the previous rebuilt spectrum
 };
 
 }  // namespace avc

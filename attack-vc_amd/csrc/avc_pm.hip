@@ -450,6 +450,11 @@ __global__ void __launch_bounds__(256) vsm_combine(VsmArgs A) {
             A.out[i] = fminf(fmaxf(acc, -1.f), 1.f);
             continue;
         }
+        if (A.mode == 2) {   // apply_weighted_constraint (utils/audio.py:77-116) of the input itself
+            const float e = f < A.low_end ? A.eps1 : (f < A.high_start ? A.eps2 : A.eps3);
+            A.out[i] = fminf(fmaxf(m, -e), e);
+            continue;
+        }
         if (A.nw > 0 && f < A.rows && t >= A.W) {
             // windows k with k*S + W <= t < k*S + W + Wo, ascending k (the reference's order)
             const int u = t - A.W;

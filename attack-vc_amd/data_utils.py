@@ -140,16 +140,38 @@ def write_wav(path: str, wav: np.ndarray, sample_rate: int) -> None:
         w.writeframes(pcm.tobytes())
 
 
+def write_wav_float(path: str, wav: np.ndarray, sample_rate: int) -> None:
+    """torchaudio.save(path, wav [C, L] float32, sr) for a .wav path: 32-bit IEEE-float WAV
+    (WAVE_FORMAT_IEEE_FLOAT, torchaudio's encoding for float32 tensors), channels interleaved."""
+    x = np.asarray(wav, np.float32)
+    if x.ndim == 1:
+        x = x[None]
+    ch = x.shape[0]
+    data = np.ascontiguousarray(x.T).astype("<f4").tobytes()
+    fmt = struct.pack("<HHIIHH", 3, ch, int(sample_rate), int(sample_rate) * 4 * ch, 4 * ch, 32)
+    fact = struct.pack("<I", x.shape[1])
+    body = b"WAVE" + b"fmt " + struct.pack("<I", len(fmt)) + fmt + b"fact" + struct.pack("<I", 4) + fact + \
+        b"data" + struct.pack("<I", len(data)) + data
+    with open(path, "wb") as f:
+        f.write(b"RIFF" + struct.pack("<I", len(body)) + body)
+
+
+def resample(x: np.ndarray, rate: int, sample_rate: int) -> np.ndarray:
+    """x at `rate` -> `sample_rate` by scipy's polyphase filter (librosa.load's resampy and
+    torchaudio's Resample filter differently: parity unpinned)."""
+    if rate == sample_rate:
+        return x
+    from math import gcd
+
+    from scipy.signal import resample_poly
+    g = gcd(int(rate), int(sample_rate))
+    return resample_poly(x, int(sample_rate) // g, int(rate) // g).astype(np.float32)
+
+
 def load_wav(audio_path: str, sample_rate: int) -> np.ndarray:
     """librosa.load(audio_path, sr=sample_rate): mono float32 at sample_rate."""
     x, rate = read_wav(audio_path)
-    if rate != sample_rate:
-        from math import gcd
-
-        from scipy.signal import resample_poly
-        g = gcd(int(rate), int(sample_rate))
-        x = resample_poly(x, int(sample_rate) // g, int(rate) // g).astype(np.float32)
-    return x
+    return resample(x, rate, sample_rate)
 
 
 def trim(wav: np.ndarray, top_db: float, frame_length: int = 2048, hop_length: int = 512):

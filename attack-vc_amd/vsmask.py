@@ -11,15 +11,18 @@ Mirrors the reference's classes with the same names, constructor arguments and d
     per-element combine in the reference's add order -> per-band clamp
     (``avc_vsmask_protect``).
 
-The mel front / back end of the reference (utils/audio.py's torchaudio MelSpectrogram,
-InverseMelScale and GriffinLim) is outside the accelerated path: protect_mel
-takes and returns the log-mel.  The reference loop as shipped cannot run (3-D mel indexed
-as 4-D; 95 predicted rows added to an 80-row mel); the settlement -- 4-D [B, 1, F, T] mel,
-predicted rows cropped to F -- is documented in include/avc.h and oracle/vsmask.py.
+The waveform entry points run utils/audio.py's converter on libavc's DSP kernels
+(audio.MelSpectrogramConverter: torchaudio MelSpectrogram / InverseMelScale / GriffinLim
+semantics, flavor 1 of avc_dsp): ``protect_file`` (vsmask.py:41-80) and ``_protect_waveform``
+(160-213) are waveform -> log-mel -> ``protect_mel`` -> waveform; ``protect_stream`` (82-158)
+replays the reference's chunk loop.  The reference as shipped cannot run (3-D mel indexed as
+4-D; 95 predicted rows added to an 80-row mel; a [1, 1, L] waveform handed to
+torchaudio.save); the settlement -- 4-D [B, 1, F, T] mel, predicted rows cropped to F, [C, L]
+waveforms -- is documented in include/avc.h and oracle/vsmask.py.
 
-CLI (mel in, mel out; .npy [1, F, T] / [B, 1, F, T] / [F, T]):
+CLI (the reference's arguments: audio in, audio out; a .npy input / output is a log-mel):
 
-  python vsmask.py --predictive_model PM.pt --header HEADER.pt --input mel.npy --output out.npy
+  python vsmask.py --predictive_model PM.pt --header HEADER.pt --input in.wav --output out.wav
 """
 import argparse
 from typing import Optional
@@ -28,6 +31,8 @@ import numpy as np
 import torch
 
 import avc_native
+import data_utils
+from audio import MelSpectrogramConverter
 from predictive_model import PredictiveModel
 
 
@@ -127,6 +132,7 @@ class VSMask:
         self.header = UniversalPerturbationHeader(device=self.device)
         if header_path is not None:
             self.header.load(header_path)
+        self.converter = MelSpectrogramConverter()
 
     def protect_mel(self, mel_spec: torch.Tensor, window_size: int = 100, future_step: int = 10,
                     epsilon1: float = 0.1, epsilon2: float = 0.05, epsilon3: float = 0.08) -> torch.Tensor:
@@ -143,19 +149,77 @@ class VSMask:
                           epsilon1, epsilon2, epsilon3)
         return out.reshape(shape)
 
-    def protect_file(self, *args, **kwargs):
-        raise NotImplementedError("protect_file needs the torchaudio mel front/back end (utils/audio.py), "
-                                  "which is outside libavc's accelerated path; use protect_mel")
+    def protect_file(self, input_path: str, output_path: str, window_size: int = 100, future_step: int = 10,
+                     epsilon1: float = 0.1, epsilon2: float = 0.05, epsilon3: float = 0.08) -> None:
+        """vsmask.py:41-80: load (channels averaged), resample to the converter's rate, protect,
+        save as a 32-bit float WAV at that rate (torchaudio.save's encoding of a float tensor)."""
+        x, rate = data_utils.read_wav(input_path)
+        sr = self.converter.sample_rate
+        x = data_utils.resample(x, rate, sr)
+        waveform = torch.from_numpy(np.ascontiguousarray(x, np.float32))[None].to(self.device)
+        protected = self._protect_waveform(waveform, window_size, future_step, epsilon1, epsilon2, epsilon3)
+        data_utils.write_wav_float(output_path, protected.cpu().numpy(), sr)
+        print(f"protected audio saved to {output_path}")
 
-    protect_stream = protect_file
+    def _protect_waveform(self, waveform: torch.Tensor, window_size: int = 100, future_step: int = 10,
+                          epsilon1: float = 0.1, epsilon2: float = 0.05, epsilon3: float = 0.08) -> torch.Tensor:
+        """vsmask.py:160-213: waveform [1, L] -> log-mel -> header + sliding-window predictions +
+        per-band clamp (protect_mel) -> Griffin-Lim waveform [1, hop * (Tf - 1)]."""
+        mel = self.converter.waveform_to_mel(waveform)            # [1, F, Tf]
+        protected = self.protect_mel(mel.unsqueeze(1), window_size, future_step, epsilon1, epsilon2, epsilon3)
+        return self.converter.mel_to_waveform(protected[:, 0])[0]
+
+    def protect_stream(self, input_stream, output_stream, window_size: int = 100, future_step: int = 10,
+                       epsilon1: float = 0.1, epsilon2: float = 0.05, epsilon3: float = 0.08) -> None:
+        """vsmask.py:82-158: `input_stream.read(window_size)` yields sample chunks until an empty
+        one.  The first chunk gets the header added to its log-mel (frames [0, min(T, Th)), no
+        clamp) and is resynthesised; every later chunk joins a buffer of at most
+        window_size // len(chunk) chunks (oldest dropped first), whose log-mel the PredictiveModel
+        predicts on (so a chunk must span a window the model takes: 25344 samples = 100 frames),
+        the prediction added from frame future_step, the difference band-clamped, and the last
+        len(chunk) samples of the resynthesis are written: `output_stream.write([1, n] array)`."""
+        buffer = []
+        header_applied = False
+        hdr = self.header.header.detach().float()
+        while True:
+            audio_chunk = input_stream.read(window_size)
+            if audio_chunk is None or len(audio_chunk) == 0:
+                break
+            chunk = torch.as_tensor(np.asarray(audio_chunk, np.float32)).reshape(1, -1).to(self.device)
+            if not header_applied:
+                chunk_mel = self.converter.waveform_to_mel(chunk)   # [1, F, Tc]
+                hl = min(chunk_mel.shape[-1], hdr.shape[-1])
+                rows = min(chunk_mel.shape[1], hdr.shape[-2])
+                chunk_mel[:, :rows, :hl] += hdr[0, 0, :rows, :hl]
+                protected_chunk = self.converter.mel_to_waveform(chunk_mel)[0]
+                header_applied = True
+            else:
+                buffer.append(chunk)
+                if len(buffer) > window_size // chunk.shape[1]:
+                    buffer.pop(0)
+                window = torch.cat(buffer, dim=1)
+                window_mel = self.converter.waveform_to_mel(window)  # [1, F, Tw]
+                with torch.no_grad():
+                    perturbation = self.predictive_model(window_mel.unsqueeze(1))
+                future_mel = window_mel.clone()
+                future_end = min(future_step + perturbation.shape[-1], future_mel.shape[-1])
+                rows = min(future_mel.shape[1], perturbation.shape[-2])
+                if future_end > future_step:
+                    future_mel[:, :rows, future_step:future_end] += perturbation[:, 0, :rows, :future_end - future_step]
+                weighted = self.converter.apply_weighted_constraint(future_mel - window_mel, epsilon1, epsilon2,
+                                                                    epsilon3)
+                future_wave = self.converter.mel_to_waveform(window_mel + weighted)[0]
+                protected_chunk = future_wave[:, -chunk.shape[1]:]
+            output_stream.write(protected_chunk.cpu().numpy())
 
 
 def main(argv=None):
-    """vsmask.py:215-264 argument names, with mel .npy files in place of audio."""
-    p = argparse.ArgumentParser(description="VSMask mel protection on MI355X")
+    """vsmask.py:215-264 arguments: --input / --output audio files (protect_file); .npy paths
+    are log-mels [F,T], [1,F,T] or [B,1,F,T] (protect_mel)."""
+    p = argparse.ArgumentParser(description="VSMask protection on MI355X")
     p.add_argument("--predictive_model", type=str, required=True)
     p.add_argument("--header", type=str, required=True)
-    p.add_argument("--input", type=str, required=True, help="log-mel .npy ([F,T], [1,F,T] or [B,1,F,T])")
+    p.add_argument("--input", type=str, required=True, help="audio file (.wav), or a log-mel .npy")
     p.add_argument("--output", type=str, required=True)
     p.add_argument("--window_size", type=int, default=100)
     p.add_argument("--future_step", type=int, default=10)
@@ -165,9 +229,12 @@ def main(argv=None):
     p.add_argument("--device", type=str, default="cuda")
     a = p.parse_args(argv)
     vs = VSMask(a.predictive_model, a.header, device=a.device)
-    mel = torch.from_numpy(np.load(a.input).astype(np.float32)).to(vs.device)
-    out = vs.protect_mel(mel, a.window_size, a.future_step, a.epsilon1, a.epsilon2, a.epsilon3)
-    np.save(a.output, out.cpu().numpy())
+    if a.input.endswith(".npy"):
+        mel = torch.from_numpy(np.load(a.input).astype(np.float32)).to(vs.device)
+        out = vs.protect_mel(mel, a.window_size, a.future_step, a.epsilon1, a.epsilon2, a.epsilon3)
+        np.save(a.output, out.cpu().numpy())
+    else:
+        vs.protect_file(a.input, a.output, a.window_size, a.future_step, a.epsilon1, a.epsilon2, a.epsilon3)
 
 
 if __name__ == "__main__":

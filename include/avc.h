@@ -259,6 +259,11 @@ int avc_header_optimize_state(avc_ctx* ctx, const float* source, const float* ta
                               int n_iters, int precision, float* losses, float* exp_avg, float* exp_avg_sq,
                               int step0, void* stream);
 
+/* MelSpectrogramConverter.apply_weighted_constraint (utils/audio.py:77-116): x [B][F][T] ->
+ * out = clamp(x, -eps, eps) with eps1 on rows [0, int(F*0.3)), eps2 to int(F*0.7), eps3 above. */
+int avc_vsmask_band_clamp(int device, const float* x, int B, int F, int T, float eps1, float eps2, float eps3,
+                          float* out, void* stream);
+
 /* UniversalPerturbationHeader.apply_header (header_model.py:70-95):
  * out = clamp(mel + header on frames [0, min(T, Th)), -1, 1). */
 int avc_vsmask_apply_header(int device, const float* mel, int B, int F, int T, const float* header, int Th,
@@ -273,6 +278,11 @@ typedef struct {
     int32_t sample_rate, n_fft, hop_length, win_length, n_mels;
     float preemph, ref_db, max_db;
     int32_t pad_mode;
+    /* 0: data_utils.py (librosa, above).  1: utils/audio.py:8-76 MelSpectrogramConverter (the
+     * VSMask converter; torchaudio semantics): MelSpectrogram power 2 with an HTK mel filter
+     * bank (norm None, f_max = sample_rate // 2), log10(clamp(., 1e-5)); preemph must be 0,
+     * ref_db / max_db unused, no mean / std; mel2wav through avc_dsp_ta_mel2wav only. */
+    int32_t flavor;
 } avc_dsp_cfg;
 typedef struct avc_dsp avc_dsp;
 int avc_dsp_create(int device, const avc_dsp_cfg* cfg, avc_dsp** out);
@@ -295,6 +305,13 @@ int avc_dsp_mel2wav(avc_dsp* dsp, const float* mel, int B, int Tf, int transpose
                     const float* std, int n_iter, float* wav, void* stream);
 /* griffin_lim(spect [B][n_fft/2+1][Tf], hop, win, n_fft, n_iter) -> wav [B][hop_length * (Tf - 1)] */
 int avc_dsp_griffin_lim(avc_dsp* dsp, const float* spect, int B, int Tf, int n_iter, float* wav, void* stream);
+/* flavor-1 context: MelSpectrogramConverter.mel_to_waveform (utils/audio.py:59-75): mel [B][n_mels][Tf]
+ * log10 mel -> pow(10, .) -> InverseMelScale (the least-squares / minimum-norm solution of
+ * fb^T X = mel, relu) -> GriffinLim(power 2, n_iter, momentum) -> wav [B][hop_length * (Tf - 1)].
+ * angles0: device [B][n_fft/2+1][Tf] complex64 initial phases (GriffinLim's rand_init draw,
+ * torch.rand(complex64)), or NULL for rand_init=False (all ones).  momentum in [0, 1). */
+int avc_dsp_ta_mel2wav(avc_dsp* dsp, const float* mel, int B, int Tf, int n_iter, float momentum,
+                       const float* angles0, float* wav, void* stream);
 /* Per-launch HIP-event profiling of a DSP context (bench.py's roofline): while enabled every
  * launch is bracketed by events on the call's stream (and synchronised); per kernel name the
  * launch count and device milliseconds accumulate.  Enabling clears the counters. */

@@ -193,3 +193,83 @@ def mel2wav(mel, sample_rate, preemph, n_fft, hop_length, win_length, n_mels, re
     mag = mel2mag(mel, sample_rate, n_fft, n_mels, ref_db, max_db)
     wav = griffin_lim(mag, hop_length, win_length, n_fft, n_iter)
     return deemphasis(wav, preemph).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------------
+# utils/audio.py's torchaudio converter (VSMask; MelSpectrogramConverter, 8-116)
+# ----------------------------------------------------------------------------------
+# torchaudio is absent from this image and /root/reference pins no version; restated from
+# torchaudio >= 2.1's published functional code: melscale_fbanks (mel_scale="htk", norm=None),
+# Spectrogram (center, reflect, power 2), InverseMelScale (torch.linalg.lstsq, then relu),
+# griffinlim (momentum, rand_init).  PARITY UNPINNED against torchaudio; the STFT / ISTFT are the
+# scipy-pinned ones above (torch.stft / istft with a Hann window and center=True compute the same
+# transforms).
+
+
+def htk_hz_to_mel(f):
+    return 2595.0 * np.log10(1.0 + np.asarray(f, np.float64) / 700.0)
+
+
+def htk_mel_to_hz(m):
+    return 700.0 * (10.0 ** (np.asarray(m, np.float64) / 2595.0) - 1.0)
+
+
+def ta_mel_fbanks(n_freqs, f_min, f_max, n_mels, sample_rate):
+    """torchaudio.functional.melscale_fbanks(norm=None, mel_scale='htk') -> [n_freqs, n_mels]."""
+    all_freqs = np.linspace(0, sample_rate // 2, n_freqs)
+    f_pts = htk_mel_to_hz(np.linspace(htk_hz_to_mel(f_min), htk_hz_to_mel(f_max), n_mels + 2))
+    f_diff = f_pts[1:] - f_pts[:-1]
+    slopes = f_pts[None, :] - all_freqs[:, None]
+    down = -slopes[:, :-2] / f_diff[:-1]
+    up = slopes[:, 2:] / f_diff[1:]
+    return np.maximum(0.0, np.minimum(down, up))
+
+
+def ta_fb(sample_rate, n_fft, n_mels):
+    """MelSpectrogram's bank: f_min 0, f_max sample_rate // 2."""
+    return ta_mel_fbanks(n_fft // 2 + 1, 0.0, float(sample_rate // 2), n_mels, sample_rate)
+
+
+def ta_wav2mel(wav, sample_rate=16000, n_fft=1024, hop_length=256, n_mels=80):
+    """utils/audio.py:44-57: log10(clamp(MelSpectrogram(wav), 1e-5)) for wav [L] -> [n_mels, Tf]."""
+    S = np.abs(stft(np.asarray(wav, np.float64), n_fft, hop_length, n_fft)) ** 2
+    return np.log10(np.maximum(ta_fb(sample_rate, n_fft, n_mels).T @ S, 1e-5))
+
+
+def ta_inverse_mel(mel_power, sample_rate=16000, n_fft=1024, n_mels=80):
+    """InverseMelScale: relu(lstsq(fb^T, mel)) (minimum-norm solution) -> [n_fft/2+1, T]."""
+    fbT = ta_fb(sample_rate, n_fft, n_mels).T
+    return np.maximum(np.linalg.lstsq(fbT, np.asarray(mel_power, np.float64), rcond=None)[0], 0.0)
+
+
+def ta_griffin_lim(spec_power, n_fft=1024, hop_length=256, n_iter=32, momentum=0.99, angles0=None):
+    """torchaudio.functional.griffinlim (power 2, center, length None): spec [F, T] -> wav."""
+    mag = np.sqrt(np.asarray(spec_power, np.float64))
+    angles = np.ones(mag.shape, np.complex128) if angles0 is None else np.asarray(angles0, np.complex128)
+    tprev = 0.0
+    for _ in range(n_iter):
+        inverse = istft(mag * angles, hop_length, n_fft)
+        rebuilt = stft(inverse, n_fft, hop_length, n_fft)
+        angles = rebuilt - tprev * (momentum / (1.0 + momentum)) if momentum else rebuilt
+        angles = angles / (np.abs(angles) + 1e-16)
+        tprev = rebuilt
+    return istft(mag * angles, hop_length, n_fft)
+
+
+def ta_mel2wav(logmel, sample_rate=16000, n_fft=1024, hop_length=256, n_mels=80, n_iter=32, momentum=0.99,
+               angles0=None):
+    """utils/audio.py:59-75 for one channel: log10 mel [n_mels, T] -> wav [hop * (T - 1)]."""
+    spec = ta_inverse_mel(10.0 ** np.asarray(logmel, np.float64), sample_rate, n_fft, n_mels)
+    return ta_griffin_lim(spec, n_fft, hop_length, n_iter, momentum, angles0)
+
+
+def band_clamp(p, eps1=0.1, eps2=0.05, eps3=0.08):
+    """utils/audio.py:77-116 along the second-to-last axis."""
+    p = np.asarray(p)
+    F = p.shape[-2]
+    lo, hi = int(F * 0.3), int(F * 0.7)
+    out = p.copy()
+    out[..., :lo, :] = np.clip(p[..., :lo, :], -eps1, eps1)
+    out[..., lo:hi, :] = np.clip(p[..., lo:hi, :], -eps2, eps2)
+    out[..., hi:, :] = np.clip(p[..., hi:, :], -eps3, eps3)
+    return out
