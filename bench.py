@@ -277,6 +277,7 @@ def main_pm(a):
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")   # host-side barrier / max only: no RCCL in the process
+    import avc_native
     import predictive_model
     import shard
     torch.manual_seed(0)
@@ -315,7 +316,8 @@ def main_pm(a):
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK["fp32"][0], "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK["fp32"][0], 4), "traffic": None,
                          "kernel": "PredictiveModel forward (pm_cin1, pm_mfma x 10, pm_cout1 + split-K pm_reduce)"},
-            "cpu_baseline": cpu, "flop_per_window": FLOP_PER_WINDOW}), flush=True)
+            "cpu_baseline": cpu, "flop_per_window": FLOP_PER_WINDOW,
+            "libavc": avc_native.lib().avc_version().decode()}), flush=True)
     if dist:
         dist.destroy_process_group()
 
@@ -349,6 +351,7 @@ def main_mel2wav(a):
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")   # host-side barrier / max only: no RCCL in the process
+    import avc_native
     import data_utils
     import shard
     B, T = a.batch, a.frames
@@ -435,7 +438,8 @@ def main_mel2wav(a):
             "config": {"workload": f"mel2wav B={B}/GPU, 80x{T} normalized mels, preprocess {PREPROCESS} "
                                    f"(assumed AdaIN-VC config)", "batch_per_gpu": B, "frames": T,
                        "parallelism": f"dp{world} (independent utterance shards, no collective)"},
-            "roofline": roof, "cpu_baseline": cpu, "front_end_wav2mel": front}), flush=True)
+            "roofline": roof, "cpu_baseline": cpu, "front_end_wav2mel": front,
+            "libavc": avc_native.lib().avc_version().decode()}), flush=True)
     if dist:
         dist.destroy_process_group()
 
