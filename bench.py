@@ -306,6 +306,10 @@ def main_pm(a):
     if rank == 0:
         value = total * steps / elapsed
         achieved = FLOP_PER_WINDOW * value / world / 1e12
+        # HBM bytes of one forward at B windows from the committed PMC passes (scripts/r03_pm_prof.sh
+        # -> profiles/r04_pm_summary.md), summed over its kernels
+        tpath = os.path.join(ROOT, "profiles", "traffic.json")
+        pm_traffic = json.load(open(tpath)).get("pm", {}).get("forward") if os.path.exists(tpath) else None
         print(json.dumps({
             "metric": "PredictiveModel windows/sec ([B,1,80,100] eval forward); 1/2/4/8 MI355X", "value": round(value, 1),
             "unit": "windows/s", "n_gpus": world, "steps": steps, "warmup": a.warmup,
@@ -314,7 +318,7 @@ def main_pm(a):
             "config": {"workload": f"PredictiveModel forward B={B}/GPU (BASELINE configs[4]; random init seed 0)",
                        "batch_per_gpu": B, "parallelism": f"dp{world} (independent window shards, no collective)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK["fp32"][0], "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK["fp32"][0], 4), "traffic": None,
+                         "frac": round(achieved / PEAK["fp32"][0], 4), "traffic": pm_traffic,
                          "kernel": "PredictiveModel forward (pm_cin1, pm_mfma x 10, pm_cout1 + split-K pm_reduce)"},
             "cpu_baseline": cpu, "flop_per_window": FLOP_PER_WINDOW,
             "libavc": avc_native.lib().avc_version().decode()}), flush=True)
