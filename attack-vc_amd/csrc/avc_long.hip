@@ -413,6 +413,77 @@ __device__ __forceinline__ void lz_in_stats(const float* raw, int Tl, int w, f32
     }
 }
 
+// Running InstanceNorm statistics of a layer computed chunk by chunk from the GEMM epilogue's
+// registers (the long Decoder): each chunk's owned frames give a count, a mean and a centred
+// second moment (two passes over registers), merged into the running ones by Chan, Golub and
+// LeVeque's pairwise update -- so no pass re-reads the raw fp32 stream for the variance (one
+// HBM read of it per IN layer instead of two).  A layer of one chunk gets exactly
+// lz_in_stats's arithmetic (the same sums in the same order).
+struct LzMom {
+    float n;
+    f32x4 mean[2], m2[2];
+};
+template <int NF, class Own>
+__device__ __forceinline__ void lz_mom_add(LzMom& M, const f32x4 (&y)[2][NF], Own own) {
+    f32x4 s[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 cnt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+        if (own(f)) {
+            s[0] += y[0][f];
+            s[1] += y[1][f];
+            cnt[0] += 1.f;
+        }
+    row16_sum(s[0]);
+    row16_sum(s[1]);
+    const float nc = row16_sum(cnt[0]);
+    if (nc == 0.f) return;
+    f32x4 mc[2], q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mc[i][r] = s[i][r] / nc;
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+        if (own(f))
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const f32x4 d = y[i][f] - mc[i];
+                q[i] += d * d;
+            }
+    row16_sum(q[0]);
+    row16_sum(q[1]);
+    if (M.n == 0.f) {
+        M.n = nc;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            M.mean[i] = mc[i];
+            M.m2[i] = q[i];
+        }
+        return;
+    }
+    const float n = M.n + nc, wa = nc / n, wb = M.n * nc / n;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float d = mc[i][r] - M.mean[i][r];
+            M.mean[i][r] += d * wa;
+            M.m2[i][r] += q[i][r] + d * d * wb;
+        }
+    M.n = n;
+}
+// mean / invstd of the merged statistics over Tl frames (biased variance, eps 1e-5); resets M
+__device__ __forceinline__ void lz_mom_get(LzMom& M, int Tl, f32x4 (&mean)[2], f32x4 (&invstd)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        mean[i] = M.mean[i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) invstd[i][r] = 1.f / sqrtf(M.m2[i][r] / (float)Tl + 1e-5f);
+    }
+    M.n = 0.f;
+}
+
 // ---------------------------------------------------------------------------------
 // forward: SpeakerEncoder (models.py:327-343) or, in ce_mode, ContentEncoder (181-210)
 // ---------------------------------------------------------------------------------
@@ -1277,7 +1348,8 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
     ring_fill(ring, op_in());
     int rb[NF];
     char* WB = fz_lds;
-    f32x4 in_s[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    LzMom mom;
+    mom.n = 0.f;
 
     lz_ct_to_img<PREC, FZ_C>(imgy, A.mu + (size_t)b * FZ_C * T0, T0);   // mu -> in_conv operand
     lz_publish();
@@ -1297,17 +1369,20 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
             f32x4 acc[2][NF];
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_in(), chk.last ? op_c1(0) : op_in(), WB, rb);
-#pragma unroll
-            for (int f = 0; f < NF; ++f) {
+            auto own = [&](int f) __attribute__((always_inline)) {
                 const int t = n0 + 16 * f + c;
-                if (t < T0 && chk.owns(t))
+                return t < T0 && chk.owns(t);
+            };
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const f32x4 y = acc[i][f] + bi[i];
-                        *lz_fl(raw, t, w, i) = y;
-                        in_s[i] += y;
-                    }
-            }
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][f] += bi[i];
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                if (own(f))
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) *lz_fl(raw, n0 + 16 * f + c, w, i) = acc[i][f];
+            lz_mom_add(mom, acc, own);
         }
     }
     // InstanceNorm over the Tl frames of raw, then out(t, i, yhat, invstd, ex) with ex = ld(t, i)
@@ -1316,7 +1391,7 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
     auto in_pass = [&](int Tl, auto&& ld, auto&& out) __attribute__((always_inline)) {
         lz_publish();
         f32x4 mean[2], inv[2];
-        lz_in_stats(raw, Tl, w, in_s, mean, inv);
+        lz_mom_get(mom, Tl, mean, inv);
         for (int F0 = 0; F0 < lz_nf(Tl); F0 += LZ_FB) {
             f32x4 v[LZ_FB][2], ex[LZ_FB][2];
 #pragma unroll
@@ -1337,7 +1412,6 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
                     for (int i = 0; i < 2; ++i) out(t, i, (v[u][i] - mean[i]) * inv[i], inv[i], ex[u][i]);
             }
         }
-        in_s[0] = in_s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
     auto no_ld = [](int, int) __attribute__((always_inline)) { return f32x4{0.f, 0.f, 0.f, 0.f}; };
     auto put_inv = [&](int q, const f32x4& inv, int i) __attribute__((always_inline)) {
@@ -1383,17 +1457,20 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c1(l), chk.last ? op_c2(l, 0) : op_c1(l), SB, rb);
             pipe1.issue_next(k, imgh, r0_w, nr_w);
-#pragma unroll
-            for (int f = 0; f < NF; ++f) {
+            auto own = [&](int f) __attribute__((always_inline)) {
                 const int t = n0 + 16 * f + c;
-                if (t < Ti && chk.owns(t))
+                return t < Ti && chk.owns(t);
+            };
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const f32x4 y = acc[i][f] + b1[i];
-                        *lz_fl(raw, t, w, i) = y;
-                        in_s[i] += y;
-                    }
-            }
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][f] += b1[i];
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                if (own(f))
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) *lz_fl(raw, n0 + 16 * f + c, w, i) = acc[i][f];
+            lz_mom_add(mom, acc, own);
         }
         float* st1 = stb + A.stash_off[2 * l];
         in_pass(Ti, no_ld, [&](int t, int i, f32x4 yh, f32x4 inv, f32x4) __attribute__((always_inline)) {
@@ -1420,17 +1497,20 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
                 const AOp nx = s + 1 < up ? op_c2(l, 1) : (chk.last ? nxt : op_c2(l, 0));
                 fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_c2(l, s), nx, SB, rb);
                 if (s + 1 == up) pipe2.issue_next(k, imgy, r0_w, nr_w);
-#pragma unroll
-                for (int f = 0; f < NF; ++f) {
+                auto own = [&](int f) __attribute__((always_inline)) {
                     const int t = n0 + 16 * f + c;
-                    if (t < Ti && chk.owns(t))
+                    return t < Ti && chk.owns(t);
+                };
 #pragma unroll
-                        for (int i = 0; i < 2; ++i) {
-                            const f32x4 y = acc[i][f] + b2[s][i];
-                            *lz_fl(raw, up * t + s, w, i) = y;
-                            in_s[i] += y;
-                        }
-                }
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) acc[i][f] += b2[s][i];
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+                    if (own(f))
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) *lz_fl(raw, up * (n0 + 16 * f + c) + s, w, i) = acc[i][f];
+                lz_mom_add(mom, acc, own);
             }
         }
         float* st2 = stb + A.stash_off[2 * l + 1];
@@ -1610,45 +1690,14 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
     //   d/dx = invstd std (g_z - (sum g_z)/n - yhat (sum g_z yhat)/n).
     // gsrc(t, i) -> g; pass 1 keeps g_z in tmp and writes d/d cond[q]; pass 2 hands
     // (t, i, d/dx) to out.
-    auto adain_in_bwd = [&](int q, int Tl, auto&& gsrc, auto&& out) __attribute__((always_inline)) {
+    // pass 2 (and the d/d cond[q] store) from the pass-1 sums gm / gs
+    auto adain_in_bwd_tail = [&](int q, int Tl, f32x4 (&gm)[2], f32x4 (&gs)[2], auto&& out) __attribute__((always_inline)) {
         const float* yq = stb + A.stash_off[q];
-        f32x4 mn[2], sd[2], is[2], gm[2], gs[2];
+        f32x4 sd[2], is[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            mn[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
             sd[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
             is[i] = *reinterpret_cast<const f32x4*>(A.invstd + ((size_t)b * 2 * nblk + q) * 128 + ch0 + 16 * i);
-            gm[i] = gs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        lz_publish();
-        // LZ_FB fragments at a time: loads, one drain, then arithmetic and stores (in_pass)
-        for (int F0 = 0; F0 < lz_nf(Tl); F0 += LZ_FB) {
-            f32x4 gv[LZ_FB][2], yv[LZ_FB][2];
-#pragma unroll
-            for (int u = 0; u < LZ_FB; ++u) {
-                const int tc = min(16 * (F0 + u) + c, Tl - 1);
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    gv[u][i] = gsrc(tc, i);
-                    yv[u][i] = lz_stash_get<PREC>(yq, tc, w, i);
-                }
-            }
-            lz_vm_drain();
-#pragma unroll
-            for (int u = 0; u < LZ_FB; ++u) {
-                const int t = 16 * (F0 + u) + c;
-                if (t < Tl)
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const f32x4 g = gv[u][i], yh = yv[u][i];
-                        f32x4 z;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) z[r] = g[r] * act_d(yh[r] * sd[i][r] + mn[i][r], act);
-                        *lz_fl(tmp, t, w, i) = z;
-                        gm[i] += z;
-                        gs[i] += z * yh;
-                    }
-            }
         }
         f32x4 k1[2], k2[2], k3[2];
         const float inv_n = 1.f / (float)Tl;
@@ -1695,6 +1744,47 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
             }
         }
     };
+    auto adain_in_bwd = [&](int q, int Tl, auto&& gsrc, auto&& out) __attribute__((always_inline)) {
+        const float* yq = stb + A.stash_off[q];
+        f32x4 mn[2], sd[2], gm[2], gs[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            mn[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + ch0 + 16 * i);
+            sd[i] = *reinterpret_cast<const f32x4*>(cond + q * 256 + 128 + ch0 + 16 * i);
+            gm[i] = gs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        lz_publish();
+        // LZ_FB fragments at a time: loads, one drain, then arithmetic and stores (in_pass)
+        for (int F0 = 0; F0 < lz_nf(Tl); F0 += LZ_FB) {
+            f32x4 gv[LZ_FB][2], yv[LZ_FB][2];
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int tc = min(16 * (F0 + u) + c, Tl - 1);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    gv[u][i] = gsrc(tc, i);
+                    yv[u][i] = lz_stash_get<PREC>(yq, tc, w, i);
+                }
+            }
+            lz_vm_drain();
+#pragma unroll
+            for (int u = 0; u < LZ_FB; ++u) {
+                const int t = 16 * (F0 + u) + c;
+                if (t < Tl)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const f32x4 g = gv[u][i], yh = yv[u][i];
+                        f32x4 z;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) z[r] = g[r] * act_d(yh[r] * sd[i][r] + mn[i][r], act);
+                        *lz_fl(tmp, t, w, i) = z;
+                        gm[i] += z;
+                        gs[i] += z * yh;
+                    }
+            }
+        }
+        adain_in_bwd_tail(q, Tl, gm, gs, out);
+    };
 
     int cur = 0;
     for (int l = nblk - 1; l >= 0; --l) {
@@ -1716,8 +1806,19 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
             lz_zero_rows<PREC>(imgg2, LZ_ZR + Ti, LZ_ZR);
         }
         lz_publish();
-        // conv2^T (both halves) over padded positions of the Ti frames -> tmp (g of conv1's output)
+        // conv2^T (both halves) over padded positions of the Ti frames = g of conv1's output, and in
+        // the same epilogue the first pass of conv1's act + AdaIN(2l) + IN backward on the chunk's
+        // owned frames: g_z -> tmp and its two row sums (the sums in the order a separate pass over
+        // the frames would take: bitwise the same, one fp32 stream write + read fewer)
         const int nfc = lz_nf(Ti + 16 + P);
+        const float* yq1 = stb + A.stash_off[2 * l];
+        f32x4 mn1[2], sd1[2], gm1[2], gs1[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            mn1[i] = *reinterpret_cast<const f32x4*>(cond + (2 * l) * 256 + ch0 + 16 * i);
+            sd1[i] = *reinterpret_cast<const f32x4*>(cond + (2 * l) * 256 + 128 + ch0 + 16 * i);
+            gm1[i] = gs1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
         LzChunk chk;
         for (int k = 0; lz_chunk(k, nfc, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
@@ -1737,6 +1838,14 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
                 const AOp nx = s + 1 < up ? op_c2T(l, 1) : (chk.last ? (l > 0 ? op_c1T(l) : op_c2T(l, 0)) : op_c2T(l, 0));
                 fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, IC<NF>{}, ring, op_c2T(l, s), nx, WB, rb);
             }
+            f32x4 yv[NF][2];   // the stash rows of the chunk's frames, loaded before any store
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = min(max(16 * (chk.f0 + f - 1) + c, 0), Ti - 1);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) yv[f][i] = lz_stash_get<PREC>(yq1, t, w, i);
+            }
+            lz_vm_drain();
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
@@ -1744,20 +1853,26 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
                 if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
                 if (t < Ti)
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) *lz_fl(gout, t, w, i) = acc[i][f];   // scratch: g of conv1's output
+                    for (int i = 0; i < 2; ++i) {
+                        const f32x4 yh = yv[f][i];
+                        f32x4 z;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) z[r] = acc[i][f][r] * act_d(yh[r] * sd1[i][r] + mn1[i][r], act);
+                        *lz_fl(tmp, t, w, i) = z;
+                        gm1[i] += z;
+                        gs1[i] += z * yh;
+                    }
             }
         }
-        // conv1 branch: act, AdaIN(2l), IN backward -> dY of conv1 (the first block stops: mu
-        // is constant in the attacks)
+        // conv1 branch: the rest of its IN backward -> dY of conv1 (the first block stops: mu is
+        // constant in the attacks)
         if (l == 0) {
-            adain_in_bwd(0, Ti, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(gout, t, w, i)); },
-                         [&](int, int, f32x4) __attribute__((always_inline)) {});
+            adain_in_bwd_tail(0, Ti, gm1, gs1, [&](int, int, f32x4) __attribute__((always_inline)) {});
             break;
         }
-        adain_in_bwd(2 * l, Ti, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(gout, t, w, i)); },
-                     [&](int t, int i, f32x4 d) __attribute__((always_inline)) {
-                         st4<PREC>(imgg + (size_t)(LZ_ZR + t) * GRB + (ch0 + 16 * i) * ESZ, d);
-                     });
+        adain_in_bwd_tail(2 * l, Ti, gm1, gs1, [&](int t, int i, f32x4 d) __attribute__((always_inline)) {
+            st4<PREC>(imgg + (size_t)(LZ_ZR + t) * GRB + (ch0 + 16 * i) * ESZ, d);
+        });
         lz_zero_rows<PREC>(imgg, 0, LZ_ZR);
         lz_zero_rows<PREC>(imgg, LZ_ZR + Ti, LZ_ZR);
         lz_publish();
