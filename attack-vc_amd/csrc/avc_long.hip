@@ -1787,18 +1787,25 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
     };
 
     int cur = 0;
+    // pass-1 sums of the next conv2 branch's IN backward, accumulated by the conv1^T epilogue
+    // that produces its input gradient (every block but the last, which starts from out_conv^T)
+    f32x4 gm2[2], gs2[2];
     for (int l = nblk - 1; l >= 0; --l) {
         const int Ti = A.Tl[l], up = A.up[l], To = Ti * up;
         float* gin = gh[cur];            // g(h_{l+1}) over To frames
         float* gout = gh[cur ^ 1];       // g(h_l) over Ti frames
         // conv2 branch: act, AdaIN(2l+1), IN backward over To frames -> dY image(s): frame
         // 2t + s of the shuffled output is half s of frame t
-        adain_in_bwd(2 * l + 1, To, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(gin, t, w, i)); },
-                     [&](int t, int i, f32x4 d) __attribute__((always_inline)) {
-                         char* im = (up == 2 && (t & 1)) ? imgg2 : imgg;
-                         const int tt = up == 2 ? t >> 1 : t;
-                         st4<PREC>(im + (size_t)(LZ_ZR + tt) * GRB + (ch0 + 16 * i) * ESZ, d);
-                     });
+        auto dy2 = [&](int t, int i, f32x4 d) __attribute__((always_inline)) {
+            char* im = (up == 2 && (t & 1)) ? imgg2 : imgg;
+            const int tt = up == 2 ? t >> 1 : t;
+            st4<PREC>(im + (size_t)(LZ_ZR + tt) * GRB + (ch0 + 16 * i) * ESZ, d);
+        };
+        if (l == nblk - 1)
+            adain_in_bwd(2 * l + 1, To, [&](int t, int i) __attribute__((always_inline)) { return f32x4(*lz_fl(gin, t, w, i)); },
+                         dy2);
+        else
+            adain_in_bwd_tail(2 * l + 1, To, gm2, gs2, dy2);
         lz_zero_rows<PREC>(imgg, 0, LZ_ZR);
         lz_zero_rows<PREC>(imgg, LZ_ZR + Ti, LZ_ZR);
         if (up == 2) {
@@ -1876,7 +1883,17 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
         lz_zero_rows<PREC>(imgg, 0, LZ_ZR);
         lz_zero_rows<PREC>(imgg, LZ_ZR + Ti, LZ_ZR);
         lz_publish();
-        // conv1^T (+ fold) + the residual branch (adjoint of the x2 nearest upsample) -> g(h_l)
+        // conv1^T (+ fold) + the residual branch (adjoint of the x2 nearest upsample) -> g(h_l),
+        // and on it the first pass of block l-1's conv2-branch IN backward (AdaIN(2l-1) over the
+        // same Ti frames): g_z -> tmp, its row sums -> gm2 / gs2
+        const float* yq2 = stb + A.stash_off[2 * l - 1];
+        f32x4 mn2[2], sd2[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            mn2[i] = *reinterpret_cast<const f32x4*>(cond + (2 * l - 1) * 256 + ch0 + 16 * i);
+            sd2[i] = *reinterpret_cast<const f32x4*>(cond + (2 * l - 1) * 256 + 128 + ch0 + 16 * i);
+            gm2[i] = gs2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
         auto r0_g = [=](const LzChunk& ch) __attribute__((always_inline)) {
             return LZ_ZR + max(16 * ch.f0 - 16, -P) + P - ks - 1;
         };
@@ -1920,6 +1937,13 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
 #pragma unroll
                     for (int i = 0; i < 2; ++i) res[f][i] = res[f][i] + r1[f][i];
             }
+            f32x4 yv[NF][2];   // block l-1's conv2-branch stash rows of the chunk's frames
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int t = min(max(16 * (chk.f0 + f - 1) + c, 0), Ti - 1);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) yv[f][i] = lz_stash_get<PREC>(yq2, t, w, i);
+            }
             lz_vm_drain();
             pipeg.issue_next(k, imgg, r0_g, nr_g);   // after the drain: it would wait for the DMA too
             lz_fold<2>(acc, chk.f0, 16, Ti, P, FSCR);
@@ -1929,7 +1953,16 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
                 if (F < 0 || 16 * F >= Ti || !chk.owns(16 * (F + 1))) continue;
                 if (t < Ti)
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) *lz_fl(gout, t, w, i) = res[f][i] + acc[i][f];
+                    for (int i = 0; i < 2; ++i) {
+                        const f32x4 g = res[f][i] + acc[i][f], yh = yv[f][i];
+                        *lz_fl(gout, t, w, i) = g;
+                        f32x4 z;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) z[r] = g[r] * act_d(yh[r] * sd2[i][r] + mn2[i][r], act);
+                        *lz_fl(tmp, t, w, i) = z;
+                        gm2[i] += z;
+                        gs2[i] += z * yh;
+                    }
             }
         }
         cur ^= 1;
