@@ -211,20 +211,39 @@ __global__ void __launch_bounds__(256) pm_cin1(PmConvArgs P) {
 // Output [B][1][Ho][Wo]
 template <int CI>
 __global__ void __launch_bounds__(256) pm_cout1(PmConvArgs P) {
+    // the workgroup's input pixels (a contiguous NHWC range: its quads' rows qy-1 .. qy), staged
+    // with coalesced 16-byte loads; pixel stride CI + 4 floats, so the 16-lane groups of a
+    // ds_read_b128 (consecutive pixels) cover the 64 banks once.  Per-lane 16-byte global reads
+    // of 128-byte pixels touched 64 cache lines per instruction: 64.6 us of the ~1.1 ms forward.
+    constexpr int XS = CI + 4, XCAP = 384;
     __shared__ float Ws[4][4 * CI];
+    __shared__ __attribute__((aligned(16))) float xs[XCAP * XS];
     for (int c = 0; c < 4; ++c) {
         const int K = CI * ((c >> 1) == 0 ? 2 : 1) * ((c & 1) == 0 ? 2 : 1);
         for (int i = threadIdx.x; i < K; i += 256) Ws[c][i] = P.w[P.woff[c] + i];
     }
-    __syncthreads();
     const int Hq = (P.Ho + 1) / 2, Wq = (P.Wo + 1) / 2;   // class (0, 0): the most blocks
-    const int N = P.B * Hq * Wq;
-    const int n = blockIdx.x * 256 + threadIdx.x;
+    const int N = P.B * Hq * Wq, HWq = Hq * Wq, HWin = P.Hin * P.Win;
+    const int n0 = blockIdx.x * 256, n1 = min(N - 1, n0 + 255);
+    const int bf = n0 / HWq, qyf = (n0 - bf * HWq) / Wq, bl = n1 / HWq, qyl = (n1 - bl * HWq) / Wq;
+    const long p_lo = (long)bf * HWin + (long)max(qyf - 1, 0) * P.Win;
+    const long p_hi = (long)bl * HWin + (long)min(qyl, P.Hin - 1) * P.Win + P.Win - 1;
+    const int cnt = (int)(p_hi - p_lo + 1);
+    const bool staged = cnt <= XCAP;                    // workgroup-uniform
+    if (staged) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(P.x + p_lo * CI);
+        for (int i = threadIdx.x; i < cnt * (CI / 4); i += 256) {
+            const int pix = i / (CI / 4), q = i - pix * (CI / 4);
+            *reinterpret_cast<f32x4*>(xs + pix * XS + 4 * q) = src[i];
+        }
+    }
+    __syncthreads();
+    const int n = n0 + threadIdx.x;
     if (n >= N) return;
-    const int b = n / (Hq * Wq);
-    const int r = n - b * Hq * Wq;
+    const int b = n / HWq;
+    const int r = n - b * HWq;
     const int qy = r / Wq, qx = r - qy * Wq;
-    const float* __restrict__ xb = P.x + (size_t)b * CI * P.Hin * P.Win;
+    const float* __restrict__ xb = P.x + (size_t)b * CI * HWin;
     // xv[dy][dx] = input (qy - dy, qx - dx), zero outside
     f32x4 xv[2][2][CI / 4];
 #pragma unroll
@@ -233,7 +252,10 @@ __global__ void __launch_bounds__(256) pm_cout1(PmConvArgs P) {
         for (int dx = 0; dx < 2; ++dx) {
             const int iy = qy - dy, ix = qx - dx;
             const bool ok = iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
-            const f32x4* src = reinterpret_cast<const f32x4*>(xb + (size_t)(ok ? iy * P.Win + ix : 0) * CI);
+            const int pi = ok ? iy * P.Win + ix : 0;
+            const int li = ok ? (int)((long)b * HWin + pi - p_lo) : 0;   // in [0, cnt) when ok
+            const f32x4* src = staged ? reinterpret_cast<const f32x4*>(xs + li * XS)
+                                      : reinterpret_cast<const f32x4*>(xb + (size_t)pi * CI);
 #pragma unroll
             for (int q = 0; q < CI / 4; ++q) xv[dy][dx][q] = ok ? src[q] : f32x4{0.f, 0.f, 0.f, 0.f};
         }
