@@ -23,6 +23,7 @@ namespace {
 constexpr int DSP_THREADS = 256;
 
 __device__ __forceinline__ int zp(int i) { return dsp_zp(i); }
+__device__ __forceinline__ int tp(int i) { return dsp_tp(i); }
 constexpr int zlen(int N) { return dsp_zlen(N); }
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
@@ -41,12 +42,12 @@ __device__ void fft_lds(float2* Z, const float2* TW, int N, int logN) {
             const int i0 = ((j >> (s - 1)) << (s + 1)) + k;
             float2 a = Z[zp(i0)], b = Z[zp(i0 + half)], c = Z[zp(i0 + 2 * half)], d = Z[zp(i0 + 3 * half)];
             // stage s: (a, b), (c, d) with W_{2 half}^k
-            const float2 w1 = TW[k * t1];
+            const float2 w1 = TW[tp(k * t1)];
             const float2 bw = cmul(b, w1), dw = cmul(d, w1);
             const float2 a1 = make_float2(a.x + bw.x, a.y + bw.y), b1 = make_float2(a.x - bw.x, a.y - bw.y);
             const float2 c1 = make_float2(c.x + dw.x, c.y + dw.y), d1 = make_float2(c.x - dw.x, c.y - dw.y);
             // stage s + 1: (a1, c1) with W_{4 half}^k, (b1, d1) with W_{4 half}^{k + half}
-            const float2 cw = cmul(c1, TW[k * t2]), dw2 = cmul(d1, TW[(k + half) * t2]);
+            const float2 cw = cmul(c1, TW[tp(k * t2)]), dw2 = cmul(d1, TW[tp((k + half) * t2)]);
             Z[zp(i0)] = make_float2(a1.x + cw.x, a1.y + cw.y);
             Z[zp(i0 + 2 * half)] = make_float2(a1.x - cw.x, a1.y - cw.y);
             Z[zp(i0 + half)] = make_float2(b1.x + dw2.x, b1.y + dw2.y);
@@ -60,7 +61,7 @@ __device__ void fft_lds(float2* Z, const float2* TW, int N, int logN) {
             const int k = j & (half - 1);
             const int i0 = ((j >> (s - 1)) << s) + k, i1 = i0 + half;
             const float2 a = Z[zp(i0)];
-            const float2 bw = cmul(Z[zp(i1)], TW[k * tstride]);
+            const float2 bw = cmul(Z[zp(i1)], TW[tp(k * tstride)]);
             Z[zp(i0)] = make_float2(a.x + bw.x, a.y + bw.y);
             Z[zp(i1)] = make_float2(a.x - bw.x, a.y - bw.y);
         }
@@ -90,7 +91,7 @@ __device__ __forceinline__ void split_pair(const float2* Z, int N, int k, float2
 
 __device__ __forceinline__ void stage_twiddles(float2* TW, const float* tw, int N) {
     for (int k = threadIdx.x; k < (N >> 1); k += DSP_THREADS)
-        TW[k] = reinterpret_cast<const float2*>(tw)[k];
+        TW[tp(k)] = reinterpret_cast<const float2*>(tw)[k];
 }
 }  // namespace
 
@@ -100,8 +101,8 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
     extern __shared__ float2 dsm[];
     const int N = A.N, F = A.F, Tf = A.Tf, L = A.L, b = blockIdx.y;
     float2* Z = dsm;                 // [zlen(N)]
-    float2* TW = Z + zlen(N);        // [N/2]
-    float* MAG = reinterpret_cast<float*>(TW + N / 2);   // [2][F]
+    float2* TW = Z + zlen(N);        // [dsp_twlen(N)]
+    float* MAG = reinterpret_cast<float*>(TW + dsp_twlen(N));   // [2][F]
     stage_twiddles(TW, A.twiddle, N);
     const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
     const float* x = A.x + (size_t)b * L;
@@ -192,7 +193,7 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
     extern __shared__ float2 dsm[];
     const int N = A.N, F = A.F, Tf = A.Tf, b = blockIdx.y, logN = A.logN, tid = threadIdx.x;
     float2* Z = dsm;                 // [zlen(N)]
-    float2* TW = Z + zlen(N);        // [N/2]
+    float2* TW = Z + zlen(N);        // [dsp_twlen(N)]
     const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
     const bool has1 = t1 < Tf;
     const float* S0 = A.spect + ((size_t)b * Tf + t0) * F;

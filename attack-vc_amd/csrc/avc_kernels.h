@@ -293,6 +293,10 @@ struct PmConvArgs {
 // 2 / 1 / 4 / 2 / 1 / 1 -- PMC: 2.85 conflict cycles per LDS instruction in the early passes)
 __host__ __device__ constexpr int dsp_zp(int i) { return i + 2 * (i >> 5) + (i >> 6); }
 __host__ __device__ constexpr int dsp_zlen(int N) { return dsp_zp(N - 1) + 1; }
+// twiddle table in LDS: one pad entry per 32, so the strided reads TW[k * (N >> s)] of the FFT
+// passes (strides 64 / 16 / 4 entries across lanes) spread over the banks instead of a few
+__host__ __device__ constexpr int dsp_tp(int i) { return i + (i >> 5); }
+__host__ __device__ constexpr int dsp_twlen(int N) { return dsp_tp(N / 2 - 1) + 1; }
 
 // UniversalPerturbationHeader.optimize (models/header_model.py:40-65), one iteration's
 // elementwise ends around the SpeakerEncoder forward / input-gradient passes
