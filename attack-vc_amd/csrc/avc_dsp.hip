@@ -9,7 +9,7 @@
 //   dsp_deemph     lfilter([1], [1, -preemph]) (161) as a one-pass tiled affine scan
 // STFT frames are the bandwidth unit: every frame kernel is one workgroup per PAIR of
 // real frames, packed as the real / imaginary parts of one complex N-point FFT
-// (radix-4 DIT passes, bit-reversed load into LDS, twiddles staged in LDS) and separated with
+// (Stockham radix-8 passes in LDS, natural order, twiddles staged in LDS) and separated with
 // the conjugate-symmetry identities; the inverse transform of two Hermitian spectra is
 // the same FFT run on conj(X0 + i X1).  HBM traffic per Griffin-Lim iteration and frame:
 // the frame written once (N floats) and read by dsp_ola, the signal read back through L2.
@@ -30,46 +30,94 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
-// in-place DIT FFT of Z[N] (input already in bit-reversed order), forward sign: pairs of
-// radix-2 stages fused into one radix-4 pass (4 LDS reads / writes per 4 butterflies, one
-// barrier per pass), a final radix-2 pass when log2 N is odd
-__device__ void fft_lds(float2* Z, const float2* TW, int N, int logN) {
-    int s = 1;
-    for (; s + 1 <= logN; s += 2) {
-        const int half = 1 << (s - 1), t1 = N >> s, t2 = N >> (s + 1);
-        for (int j = threadIdx.x; j < (N >> 2); j += DSP_THREADS) {
-            const int k = j & (half - 1);
-            const int i0 = ((j >> (s - 1)) << (s + 1)) + k;
-            float2 a = Z[zp(i0)], b = Z[zp(i0 + half)], c = Z[zp(i0 + 2 * half)], d = Z[zp(i0 + 3 * half)];
-            // stage s: (a, b), (c, d) with W_{2 half}^k
-            const float2 w1 = TW[tp(k * t1)];
-            const float2 bw = cmul(b, w1), dw = cmul(d, w1);
-            const float2 a1 = make_float2(a.x + bw.x, a.y + bw.y), b1 = make_float2(a.x - bw.x, a.y - bw.y);
-            const float2 c1 = make_float2(c.x + dw.x, c.y + dw.y), d1 = make_float2(c.x - dw.x, c.y - dw.y);
-            // stage s + 1: (a1, c1) with W_{4 half}^k, (b1, d1) with W_{4 half}^{k + half}
-            const float2 cw = cmul(c1, TW[tp(k * t2)]), dw2 = cmul(d1, TW[tp((k + half) * t2)]);
-            Z[zp(i0)] = make_float2(a1.x + cw.x, a1.y + cw.y);
-            Z[zp(i0 + 2 * half)] = make_float2(a1.x - cw.x, a1.y - cw.y);
-            Z[zp(i0 + half)] = make_float2(b1.x + dw2.x, b1.y + dw2.y);
-            Z[zp(i0 + 3 * half)] = make_float2(b1.x - dw2.x, b1.y - dw2.y);
+// Forward FFT of Z[N] in place, natural order in and out: Stockham auto-sort passes of radix 8
+// (then one of 4 or 2), each thread one or two butterflies per pass -- its R inputs at stride
+// N/R (consecutive across lanes: conflict-free reads), the twiddles W_{R Ns}^{k m} from the
+// padded table (W^(e + N/2) = -W^e), an in-register radix-R DFT, a barrier, the R outputs to
+// (j / Ns) R Ns + j % Ns + r Ns, a barrier.  2048 points: 4 passes of 16-22 LDS accesses per
+// thread (the radix-4 DIT with bit-reversed input took 6 passes and ~130, with 8-32-way
+// conflicted strided twiddle and butterfly accesses: 1.9 bank-conflict cycles per LDS cycle).
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }   // -i a
+
+template <int R>
+__device__ __forceinline__ void dft_r(float2 (&a)[R]) {
+    if constexpr (R == 2) {
+        const float2 t = a[0];
+        a[0] = cadd(t, a[1]);
+        a[1] = csub(t, a[1]);
+    } else if constexpr (R == 4) {
+        const float2 t0 = cadd(a[0], a[2]), t1 = csub(a[0], a[2]), t2 = cadd(a[1], a[3]),
+                     t3 = mul_mi(csub(a[1], a[3]));
+        a[0] = cadd(t0, t2);
+        a[1] = cadd(t1, t3);
+        a[2] = csub(t0, t2);
+        a[3] = csub(t1, t3);
+    } else {   // R == 8: one radix-2 DIF stage (W8^m on the differences), two radix-4 DFTs
+        constexpr float S2 = 0.70710678118654752f;
+        float2 u[4], v[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            u[m] = cadd(a[m], a[m + 4]);
+            v[m] = csub(a[m], a[m + 4]);
         }
-        __syncthreads();
-    }
-    if (s == logN) {
-        const int half = 1 << (s - 1), tstride = N >> s;
-        for (int j = threadIdx.x; j < (N >> 1); j += DSP_THREADS) {
-            const int k = j & (half - 1);
-            const int i0 = ((j >> (s - 1)) << s) + k, i1 = i0 + half;
-            const float2 a = Z[zp(i0)];
-            const float2 bw = cmul(Z[zp(i1)], TW[tp(k * tstride)]);
-            Z[zp(i0)] = make_float2(a.x + bw.x, a.y + bw.y);
-            Z[zp(i1)] = make_float2(a.x - bw.x, a.y - bw.y);
+        v[1] = make_float2((v[1].x + v[1].y) * S2, (v[1].y - v[1].x) * S2);
+        v[2] = mul_mi(v[2]);
+        v[3] = make_float2((v[3].y - v[3].x) * S2, -(v[3].x + v[3].y) * S2);
+        dft_r<4>(u);
+        dft_r<4>(v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            a[2 * r] = u[r];
+            a[2 * r + 1] = v[r];
         }
-        __syncthreads();
     }
 }
 
-__device__ __forceinline__ int bitrev(int n, int logN) { return (int)(__brev((unsigned)n) >> (32 - logN)); }
+template <int R, int LR, int LOGN, int LOGNS>
+__device__ __forceinline__ void fft_pass(float2* Z, const float2* TW) {
+    constexpr int N = 1 << LOGN, NB = N >> LR, NS = 1 << LOGNS, SH = LOGN - LOGNS - LR;
+    constexpr int U = NB > DSP_THREADS ? NB / DSP_THREADS : 1;   // butterflies per thread
+    float2 a[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int j = threadIdx.x + DSP_THREADS * u;
+        if (NB < DSP_THREADS && j >= NB) continue;
+        const int k = j & (NS - 1);
+#pragma unroll
+        for (int m = 0; m < R; ++m) a[u][m] = Z[zp(j + m * NB)];
+#pragma unroll
+        for (int m = 1; m < R; ++m) {
+            const int e = (k * m) << SH;
+            float2 t = TW[tp(e & (N / 2 - 1))];
+            if (e >= N / 2) t = make_float2(-t.x, -t.y);
+            a[u][m] = cmul(a[u][m], t);
+        }
+        dft_r<R>(a[u]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int j = threadIdx.x + DSP_THREADS * u;
+        if (NB < DSP_THREADS && j >= NB) continue;
+        const int idx = ((j >> LOGNS) << (LOGNS + LR)) + (j & (NS - 1));
+#pragma unroll
+        for (int r = 0; r < R; ++r) Z[zp(idx + r * NS)] = a[u][r];
+    }
+    __syncthreads();
+}
+
+// radix 8 while three or more factors of two remain, then one pass of 4 or 2 (compile-time
+// n_fft: each kernel is instantiated per log2 n_fft, so the registers are those of its passes)
+template <int LOGN, int LOGNS = 0>
+__device__ __forceinline__ void fft_lds(float2* Z, const float2* TW) {
+    if constexpr (LOGNS < LOGN) {
+        constexpr int REM = LOGN - LOGNS, LR = REM >= 3 ? 3 : REM;
+        fft_pass<1 << LR, LR, LOGN, LOGNS>(Z, TW);
+        fft_lds<LOGN, LOGNS + LR>(Z, TW);
+    }
+}
 
 // numpy.pad(mode='reflect') index into [0, L) (no edge repeat; any overhang), or -1 (constant)
 __device__ __forceinline__ int pad_index(int s, int L, int pad_mode) {
@@ -97,9 +145,11 @@ __device__ __forceinline__ void stage_twiddles(float2* TW, const float* tw, int 
 
 // grid (ceil(Tf / 2), B): frames 2p, 2p + 1 of utterance b -> mel [B][Tf][n_mels] or
 // [B][n_mels][Tf] (transpose), normalized with (mean, std) when given
+template <int LOGN>
 __global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
     extern __shared__ float2 dsm[];
-    const int N = A.N, F = A.F, Tf = A.Tf, L = A.L, b = blockIdx.y;
+    constexpr int N = 1 << LOGN;
+    const int F = A.F, Tf = A.Tf, L = A.L, b = blockIdx.y;
     float2* Z = dsm;                 // [zlen(N)]
     float2* TW = Z + zlen(N);        // [dsp_twlen(N)]
     float* MAG = reinterpret_cast<float*>(TW + dsp_twlen(N));   // [2][F]
@@ -116,10 +166,10 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
     };
     for (int n = threadIdx.x; n < N; n += DSP_THREADS) {
         const float w = A.window[n];
-        Z[zp(bitrev(n, A.logN))] = make_float2(sample(t0, n) * w, sample(t1, n) * w);
+        Z[zp(n)] = make_float2(sample(t0, n) * w, sample(t1, n) * w);
     }
     __syncthreads();
-    fft_lds(Z, TW, N, A.logN);
+    fft_lds<LOGN>(Z, TW);
     for (int k = threadIdx.x; k < F; k += DSP_THREADS) {
         float2 X0, X1;
         split_pair(Z, N, k, X0, X1);
@@ -185,13 +235,15 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_transpose(DspArgs A) {
 // grid (ceil(Tf / 2), B): one Griffin-Lim step for frames 2p, 2p + 1 (data_utils.py:190-195):
 //   init: X = S;  else X = S * est / max(1e-8, |est|), est = STFT(y) (center, pad_mode)
 //   frames[t] = window * irfft(X[:, t])
+template <int LOGN>
 __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
-    // bins per thread: k = tid + 256 i, i < KPT covers F = N/2 + 1 <= 2049 (N <= 4096);
+    // bins per thread: k = tid + 256 i, i < KPT covers F = N/2 + 1;
     // both spectra stay in registers between the forward and inverse transforms, so the
     // LDS holds only the FFT buffer and the twiddles (more workgroups per CU)
-    constexpr int KPT = (4096 / 2 + 1 + DSP_THREADS - 1) / DSP_THREADS;
+    constexpr int N = 1 << LOGN;
+    constexpr int KPT = (N / 2 + 1 + DSP_THREADS - 1) / DSP_THREADS;
     extern __shared__ float2 dsm[];
-    const int N = A.N, F = A.F, Tf = A.Tf, b = blockIdx.y, logN = A.logN, tid = threadIdx.x;
+    const int F = A.F, Tf = A.Tf, b = blockIdx.y, tid = threadIdx.x;
     float2* Z = dsm;                 // [zlen(N)]
     float2* TW = Z + zlen(N);        // [dsp_twlen(N)]
     const int t0 = 2 * blockIdx.x, t1 = t0 + 1;
@@ -237,11 +289,11 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
             const int s1 = pad_index(t1 * A.hop + n - N / 2, A.L, A.pad_mode);
             const float v0 = s0 < 0 ? 0.f : y[s0];
             const float v1 = (!has1 || s1 < 0) ? 0.f : y[s1];
-            Z[zp(bitrev(n, logN))] = make_float2(v0 * w, v1 * w);
+            Z[zp(n)] = make_float2(v0 * w, v1 * w);
         }
         stage_twiddles(TW, A.twiddle, N);
         __syncthreads();
-        fft_lds(Z, TW, N, logN);
+        fft_lds<LOGN>(Z, TW);
 #pragma unroll
         for (int i = 0; i < KPT; ++i) {
             const int k = tid + DSP_THREADS * i;
@@ -273,7 +325,7 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
     }
     __syncthreads();   // every read of the forward spectrum is done
     // conj(X0 + i X1) over the full Hermitian extension (bins k and N - k from the same
-    // thread), bit-reversed; irfft ignores the imaginary parts of the DC and Nyquist bins
+    // thread), in natural order; irfft ignores the imaginary parts of the DC and Nyquist bins
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
         const int k = tid + DSP_THREADS * i;
@@ -281,13 +333,13 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
             float2 a = X0[i], c = X1[i];
             if (k == 0 || k == N / 2) a.y = c.y = 0.f;
             // Z = X0 + i X1 = (X0.x - X1.y) + i (X0.y + X1.x); store conj(Z)
-            Z[zp(bitrev(k, logN))] = make_float2(a.x - c.y, -(a.y + c.x));
+            Z[zp(k)] = make_float2(a.x - c.y, -(a.y + c.x));
             if (k != 0 && k != N / 2)   // bin N - k: conj(X0) + i conj(X1)
-                Z[zp(bitrev(N - k, logN))] = make_float2(a.x + c.y, a.y - c.x);
+                Z[zp(N - k)] = make_float2(a.x + c.y, a.y - c.x);
         }
     }
     __syncthreads();
-    fft_lds(Z, TW, N, logN);
+    fft_lds<LOGN>(Z, TW);
     // z = conj(FFT(conj Z)) / N: frame0 = Re z, frame1 = Im z
     const float invN = 1.f / (float)N;
     float* f0 = A.frames + ((size_t)b * Tf + t0) * N;
@@ -383,5 +435,12 @@ __global__ void __launch_bounds__(1024) dsp_deemph(DspArgs A) {
         __syncthreads();
     }
 }
+
+#define AVC_DSP_INST(LG)                                          \
+    template __global__ void dsp_wav2mel<LG>(DspArgs);            \
+    template __global__ void dsp_gl_frames<LG>(DspArgs);
+AVC_DSP_INST(4) AVC_DSP_INST(5) AVC_DSP_INST(6) AVC_DSP_INST(7) AVC_DSP_INST(8)
+AVC_DSP_INST(9) AVC_DSP_INST(10) AVC_DSP_INST(11) AVC_DSP_INST(12)
+#undef AVC_DSP_INST
 
 }  // namespace avc

@@ -291,7 +291,9 @@ struct PmConvArgs {
 // groups of every access pattern at N = 2048 (worst extra-cycle factor per instruction:
 // bit-reversed store 1, radix-4 passes 1 / 2 / 2 / 1 / 1; the former one-per-32 pad had
 // 2 / 1 / 4 / 2 / 1 / 1 -- PMC: 2.85 conflict cycles per LDS instruction in the early passes)
-__host__ __device__ constexpr int dsp_zp(int i) { return i + 2 * (i >> 5) + (i >> 6); }
+// FFT buffer padding: one pad entry per 8 -- the Stockham passes' stride-8 output writes
+// (radix 8 at sub-transform size 1) then cover 32 distinct bank pairs per 32 lanes
+__host__ __device__ constexpr int dsp_zp(int i) { return i + (i >> 3); }
 __host__ __device__ constexpr int dsp_zlen(int N) { return dsp_zp(N - 1) + 1; }
 // twiddle table in LDS: one pad entry per 32, so the strided reads TW[k * (N >> s)] of the FFT
 // passes (strides 64 / 16 / 4 entries across lanes) spread over the banks instead of a few
