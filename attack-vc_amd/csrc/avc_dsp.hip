@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "avc_kernels.h"
+#include "avc_device.h"
 
 namespace avc {
 
@@ -349,6 +350,41 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
         f0[n] = z.x * w;
         if (has1) f0[N + n] = -z.y * w;
     }
+}
+
+// grid (ceil(Ly / 256)): wss[j] = sum over the frames t covering s = j + N/2 of window[s - t*hop]^2,
+// once per call (the same sum, in the same order, that dsp_ola computed per sample and iteration)
+__global__ void __launch_bounds__(DSP_THREADS) dsp_wss(DspArgs A) {
+    const int j = blockIdx.x * DSP_THREADS + threadIdx.x;
+    if (j >= A.Ly) return;
+    const int N = A.N, hop = A.hop, s = j + N / 2;
+    const int tlo = s - N + 1 <= 0 ? 0 : (s - N + hop) / hop, thi = min(A.Tf - 1, s / hop);
+    float wss = 0.f;
+    for (int t = tlo; t <= thi; ++t) {
+        const float w = A.window[s - t * hop];
+        wss += w * w;
+    }
+    A.wss[j] = wss;
+}
+
+// grid (ceil(Ly / 1024), B) when hop % 4 == 0: four consecutive samples per thread.  With N/2 and
+// hop multiples of 4, the four samples' positions n..n+3 in a frame are all inside it or all
+// outside, so each covering frame is one 16-byte load; per sample the frames are summed in the
+// same (ascending) order as dsp_ola, and divided by the precomputed window sum-square.
+__global__ void __launch_bounds__(DSP_THREADS) dsp_ola4(DspArgs A) {
+    const int j = 4 * (blockIdx.x * DSP_THREADS + threadIdx.x), b = blockIdx.y;
+    if (j >= A.Ly) return;
+    const int N = A.N, hop = A.hop, s = j + N / 2;
+    const int tlo = s - N + 4 <= 0 ? 0 : (s - N + 3 + hop) / hop, thi = min(A.Tf - 1, s / hop);
+    const float* fr = A.frames + (size_t)b * A.Tf * N;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int t = tlo; t <= thi; ++t) acc += *reinterpret_cast<const f32x4*>(fr + (size_t)t * N + (s - t * hop));
+    const f32x4 w = *reinterpret_cast<const f32x4*>(A.wss + j);
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = w[e] > 1.17549435e-38f ? acc[e] / w[e] : acc[e];
+    *reinterpret_cast<f32x4*>(A.y + (size_t)b * A.Ly + j) = y;
 }
 
 // grid (ceil(Ly / 256), B): y[j] = sum_t frames[t][s - t*hop] / wss[s], s = j + N/2

@@ -357,6 +357,7 @@ struct DspArgs {
     float* frames;                     // [B][Tf][N] windowed inverse-FFT frames
     float* y;                          // [B][Ly] overlap-added signal
     float* wav;                        // [B][Ly] de-emphasised output
+    float* wss;                        // [Ly] window sum-square of the output samples (dsp_wss)
     // flavor 1: utils/audio.py's torchaudio converter (power-2 STFT, log10 mel, pinv inverse,
     // Griffin-Lim with momentum from given initial angles); 0: data_utils.py's librosa pipeline
     int32_t flavor;
