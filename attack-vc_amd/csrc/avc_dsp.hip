@@ -284,13 +284,43 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
         stage_twiddles(TW, A.twiddle, N);
     } else {
         const float* y = A.y + (size_t)b * A.L;
-        for (int n = tid; n < N; n += DSP_THREADS) {
-            const float w = A.window[n];
-            const int s0 = pad_index(t0 * A.hop + n - N / 2, A.L, A.pad_mode);
-            const int s1 = pad_index(t1 * A.hop + n - N / 2, A.L, A.pad_mode);
-            const float v0 = s0 < 0 ? 0.f : y[s0];
-            const float v1 = (!has1 || s1 < 0) ? 0.f : y[s1];
-            Z[zp(n)] = make_float2(v0 * w, v1 * w);
+        if (A.vec4) {   // hop, L and y 16-byte aligned: four samples per 16-byte load off the edges
+            for (int n = 4 * tid; n < N; n += 4 * DSP_THREADS) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(A.window + n);
+                const int b0 = t0 * A.hop + n - N / 2, b1 = t1 * A.hop + n - N / 2;
+                f32x4 v0, v1;
+                if (b0 >= 0 && b0 + 3 < A.L) {
+                    v0 = *reinterpret_cast<const f32x4*>(y + b0);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int s0 = pad_index(b0 + e, A.L, A.pad_mode);
+                        v0[e] = s0 < 0 ? 0.f : y[s0];
+                    }
+                }
+                if (!has1) {
+                    v1 = f32x4{0.f, 0.f, 0.f, 0.f};
+                } else if (b1 >= 0 && b1 + 3 < A.L) {
+                    v1 = *reinterpret_cast<const f32x4*>(y + b1);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int s1 = pad_index(b1 + e, A.L, A.pad_mode);
+                        v1[e] = s1 < 0 ? 0.f : y[s1];
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Z[zp(n + e)] = make_float2(v0[e] * w[e], v1[e] * w[e]);
+            }
+        } else {
+            for (int n = tid; n < N; n += DSP_THREADS) {
+                const float w = A.window[n];
+                const int s0 = pad_index(t0 * A.hop + n - N / 2, A.L, A.pad_mode);
+                const int s1 = pad_index(t1 * A.hop + n - N / 2, A.L, A.pad_mode);
+                const float v0 = s0 < 0 ? 0.f : y[s0];
+                const float v1 = (!has1 || s1 < 0) ? 0.f : y[s1];
+                Z[zp(n)] = make_float2(v0 * w, v1 * w);
+            }
         }
         stage_twiddles(TW, A.twiddle, N);
         __syncthreads();
@@ -344,11 +374,17 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_gl_frames(DspArgs A) {
     // z = conj(FFT(conj Z)) / N: frame0 = Re z, frame1 = Im z
     const float invN = 1.f / (float)N;
     float* f0 = A.frames + ((size_t)b * Tf + t0) * N;
-    for (int n = tid; n < N; n += DSP_THREADS) {
-        const float w = A.window[n] * invN;
-        const float2 z = Z[zp(n)];
-        f0[n] = z.x * w;
-        if (has1) f0[N + n] = -z.y * w;
+    for (int n = 4 * tid; n < N; n += 4 * DSP_THREADS) {   // N >= 16: four per thread, 16-byte stores
+        f32x4 w = *reinterpret_cast<const f32x4*>(A.window + n), o0, o1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float2 z = Z[zp(n + e)];
+            w[e] = w[e] * invN;
+            o0[e] = z.x * w[e];
+            o1[e] = -z.y * w[e];
+        }
+        *reinterpret_cast<f32x4*>(f0 + n) = o0;
+        if (has1) *reinterpret_cast<f32x4*>(f0 + N + n) = o1;
     }
 }
 

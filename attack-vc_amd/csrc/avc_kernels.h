@@ -358,6 +358,7 @@ struct DspArgs {
     float* y;                          // [B][Ly] overlap-added signal
     float* wav;                        // [B][Ly] de-emphasised output
     float* wss;                        // [Ly] window sum-square of the output samples (dsp_wss)
+    int32_t vec4;                      // hop % 4 == 0 and y 16-byte aligned: 16-byte sample accesses
     // flavor 1: utils/audio.py's torchaudio converter (power-2 STFT, log10 mel, pinv inverse,
     // Griffin-Lim with momentum from given initial angles); 0: data_utils.py's librosa pipeline
     int32_t flavor;
