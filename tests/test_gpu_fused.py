@@ -149,6 +149,42 @@ def test_bf16_objective_after_1500(full):
     assert float(((l16 - l32).abs() / l32).max()) <= 0.05, (l16, l32)
 
 
+def test_bf16_vs_fp32_at_bench_size(full):
+    """The headline configuration itself (BASELINE configs[1]: B=256, T=128, n_iters=1500, eps=0.1):
+    the bf16 attack against the fp32 one (the reference's arithmetic) over all 256 utterances.
+    Element-wise the two adv tensors drift apart (Adam normalises every element's step, so elements
+    with near-zero gradients wander; bench.py reports max |adv16 - adv32| ~ 0.11 of the 2 eps range),
+    so the check is on what the attack is for: every utterance's objective MSE(SE(adv), SE(adv_tgt))
+    decreases under both, and the bf16 objective is close to the fp32 one (thresholds ~4x the
+    distribution observed on MI355X, printed)."""
+    z, m, ctx = full
+    ctx.set_engine("fused")
+    g = torch.Generator().manual_seed(256)
+    vc, at, p0 = (torch.randn(256, 80, 128, generator=g).to(DEV) for _ in range(3))
+    a32, _, _ = ctx.emb_attack(vc, at, p0, 0.1, 1500)
+    a16, _, _ = ctx.emb_attack(vc, at, p0, 0.1, 1500, precision="bf16")
+    ctx.set_engine("auto")
+    assert float((a16 - vc).abs().max()) <= 0.1 + 1e-6 and float((a32 - vc).abs().max()) <= 0.1 + 1e-6
+    tgt = ctx.se_forward(at)
+    l0 = ((ctx.se_forward(vc) - tgt) ** 2).mean(1)
+    l32 = ((ctx.se_forward(a32) - tgt) ** 2).mean(1)
+    l16 = ((ctx.se_forward(a16) - tgt) ** 2).mean(1)
+    rel = ((l16 - l32).abs() / l32).cpu()
+    d = (a16 - a32).abs().flatten().cpu()
+    q = torch.quantile(rel, torch.tensor([0.5, 0.9, 0.99]))
+    qe = torch.quantile(d[torch.randperm(d.numel(), generator=torch.Generator().manual_seed(0))[:1000000]],
+                        torch.tensor([0.5, 0.99, 0.999]))
+    print(f"objective rel diff median {q[0]:.4f} p90 {q[1]:.4f} p99 {q[2]:.4f} max {rel.max():.4f}; "
+          f"|adv16-adv32| median {qe[0]:.2e} p99 {qe[1]:.2e} p99.9 {qe[2]:.2e} max {d.max():.3f}; "
+          f"objective decrease fp32 {float((l32 / l0).mean()):.3f} bf16 {float((l16 / l0).mean()):.3f}")
+    assert (l32 < l0).all() and (l16 < l0).all()
+    # observed on MI355X: rel diff median 0.0022, p99 0.0093, max 0.0112; |adv16 - adv32| median
+    # 4.3e-4, p99.9 0.024; mean objective ratio 0.244 under both
+    assert float(q[0]) <= 0.01 and float(rel.max()) <= 0.05
+    assert float(qe[0]) <= 2e-3
+    assert abs(float((l16 / l0).mean()) - float((l32 / l0).mean())) <= 0.01
+
+
 def test_fused_head_matches_separate_head(full, monkeypatch):
     """The bf16 emb attack runs the head chain (dense blocks, output Linear, loss and its
     backward) inside se_fwd_fused (se_head_fused); AVC_FUSE_HEAD=0 plans the separate
