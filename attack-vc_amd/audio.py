@@ -11,7 +11,9 @@ torchaudio's semantics:
     fb^T X = mel: the minimum-norm least-squares solution for the full-rank bank, as one pinv
     matrix; relu), ``GriffinLim(n_fft, hop_length)`` with torchaudio's defaults: power 2, 32
     iterations, momentum 0.99, random initial phases drawn exactly as torchaudio draws them
-    (``torch.rand(shape, dtype=complex64, device=...)``, so a seeded run takes the same draw).
+    (``torch.rand(shape, dtype=complex64)`` on the CPU generator -- the reference's converter modules are
+    never moved to a device, so utils/audio.py only runs on CPU and draws there; the draw is then moved
+    to the GPU, so a seeded run takes the reference's draw).
   * ``apply_weighted_constraint`` (77-116): the per-band clamp (``avc_vsmask_band_clamp``).
 
 torchaudio is absent here, so these numerics are restated from its published algorithms
@@ -77,8 +79,8 @@ class MelSpectrogramConverter:
             raise RuntimeError(f"expected a log-mel [C, {self.n_mels}, T], got {tuple(mel_spec.shape)}")
         C, _, T = m.shape
         angles0 = None
-        if self.rand_init:   # torchaudio.functional.griffinlim's draw (same shape, dtype, device)
-            angles0 = torch.rand((C, self.n_fft // 2 + 1, T), dtype=torch.complex64, device=m.device)
+        if self.rand_init:   # torchaudio.functional.griffinlim's draw (same shape and dtype, CPU generator)
+            angles0 = torch.rand((C, self.n_fft // 2 + 1, T), dtype=torch.complex64).to(m.device)
         wav = self._ctx(m.device).ta_mel2wav(m.contiguous(), self.n_iter, self.momentum, angles0)
         return wav.unsqueeze(0)
 

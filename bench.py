@@ -306,10 +306,12 @@ def main_pm(a):
     if rank == 0:
         value = total * steps / elapsed
         achieved = FLOP_PER_WINDOW * value / world / 1e12
-        # HBM bytes of one forward at B windows from the committed PMC passes (scripts/r03_pm_prof.sh
-        # -> profiles/r04_pm_summary.md), summed over its kernels
+        # HBM bytes of one forward from the committed PMC passes (scripts/r03_pm_prof.sh ->
+        # profiles/r04_pm_summary.md), summed over its kernels -- measured at one batch size, so reported
+        # only when this run's per-GPU batch is that one (null otherwise)
         tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        pm_traffic = json.load(open(tpath)).get("pm", {}).get("forward") if os.path.exists(tpath) else None
+        pm_rec = json.load(open(tpath)).get("pm", {}) if os.path.exists(tpath) else {}
+        pm_traffic = pm_rec.get("forward") if pm_rec.get("batch") == B else None
         print(json.dumps({
             "metric": "PredictiveModel windows/sec ([B,1,80,100] eval forward); 1/2/4/8 MI355X", "value": round(value, 1),
             "unit": "windows/s", "n_gpus": world, "steps": steps, "warmup": a.warmup,

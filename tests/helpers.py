@@ -103,3 +103,30 @@ def rel(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def oracle_grad0_instrumented(kind, w, cfg, src, vc, at, p0, flip=None):
+    """The oracle's iteration-0 gradient of a `kind` attack (float64 weights/inputs for the
+    calibration tests) with every ReLU call numbered in call order.  Returns (grad0, pre): pre[i]
+    is call i's pre-activation.  flip=(i, idx) inverts call i's ReLU mask at element idx (forward
+    and backward: the oracle's act' reads the post-activation), i.e. the other branch of a unit
+    whose pre-activation is within rounding of zero.  Test infrastructure for
+    test_gpu_vc_full.py::test_fb_grad0_drift_is_one_relu_flip."""
+    pre = []
+
+    def relu(x):
+        i = len(pre)
+        pre.append(x)
+        m = x > 0
+        if flip is not None and flip[0] == i:
+            m = m.copy()
+            m[flip[1]] = ~m[flip[1]]
+        return np.where(m, x, 0)
+    orig = oracle.acts
+    oracle.acts = lambda c: (relu, (lambda y: (y > 0).astype(y.dtype)))
+    try:
+        rec = {}
+        oracle.attack(kind, w, cfg, src, vc, at, 0.1, 1, p0, record=rec)
+    finally:
+        oracle.acts = orig
+    return rec["grad0"], pre

@@ -81,7 +81,7 @@ def test_mel_to_waveform_32_iterations_quality():
     wav = c.mel_to_waveform(torch.from_numpy(logmel)[None].to(DEV))
     assert wav.shape == (1, 1, HOP * (logmel.shape[-1] - 1))
     torch.manual_seed(11)
-    a0 = torch.rand((1, NFFT // 2 + 1, logmel.shape[-1]), dtype=torch.complex64, device=DEV)
+    a0 = torch.rand((1, NFFT // 2 + 1, logmel.shape[-1]), dtype=torch.complex64)   # CPU generator
     ref = mel_dsp.ta_mel2wav(logmel, SR, NFFT, HOP, NMEL, 32, 0.99, a0[0].cpu().numpy())
     S = np.sqrt(mel_dsp.ta_inverse_mel(10.0 ** logmel.astype(np.float64), SR, NFFT, NMEL))
 
@@ -90,7 +90,8 @@ def test_mel_to_waveform_32_iterations_quality():
     dg, dr = dist(wav[0, 0].cpu().numpy()), dist(ref)
     print(f"spectral distance after 32 iterations: gpu {dg:.4f} oracle {dr:.4f}")
     assert dg <= dr * 1.05 + 1e-3
-    # the draw is torchaudio's: the same seed gives the same waveform
+    # the initial phases come from the CPU generator (where the reference's CPU-only converter draws
+    # them): the same seed gives the same waveform
     torch.manual_seed(11)
     again = c.mel_to_waveform(torch.from_numpy(logmel)[None].to(DEV))
     assert torch.equal(again, wav)
@@ -178,3 +179,42 @@ def test_protect_stream():
     assert w.chunks[0].shape == (1, HOP * (1 + W // HOP - 1))          # header chunk: its own resynthesis
     assert [c.shape for c in w.chunks[1:]] == [(1, W), (1, W), (1, 5000)]
     assert all(np.isfinite(c).all() for c in w.chunks)
+
+
+def test_protect_stream_equals_composition():
+    """protect_stream (vsmask.py:82-158) recomputed by hand under the same seed, every written chunk
+    bitwise: the header-only first chunk (header added to frames [0, min(T, Th)), no clamp), then per
+    later chunk its window's log-mel, the PredictiveModel forward, the prediction added from frame
+    future_step, the band clamp of future_mel - window_mel and the resynthesis's last len(chunk)
+    samples.  Also: the clamped perturbation is zero before future_step and lands after it."""
+    vs = _vsmask(4)
+    W, fs = 99 * HOP, 10
+    x = _signal(3 * W, 8)
+    r, w = _Reader(x), _Writer()
+    torch.manual_seed(9)
+    vs.protect_stream(r, w, window_size=W, future_step=fs)
+    assert len(w.chunks) == 3
+    torch.manual_seed(9)                           # one Griffin-Lim phase draw per chunk, in order
+    hdr = vs.header.header.detach().float()
+    c0 = torch.from_numpy(x[:W])[None].to(DEV)
+    m0 = vs.converter.waveform_to_mel(c0)
+    hl, rows = min(m0.shape[-1], hdr.shape[-1]), min(m0.shape[1], hdr.shape[-2])
+    m0h = m0.clone()
+    m0h[:, :rows, :hl] = m0h[:, :rows, :hl] + hdr[0, 0, :rows, :hl]
+    assert np.array_equal(w.chunks[0], vs.converter.mel_to_waveform(m0h)[0].cpu().numpy())
+    for k in (1, 2):                               # buffer holds W // W = 1 chunk: the window is the chunk
+        ck = torch.from_numpy(x[k * W:(k + 1) * W])[None].to(DEV)
+        wm = vs.converter.waveform_to_mel(ck)
+        with torch.no_grad():
+            pred = vs.predictive_model(wm.unsqueeze(1))
+        fut = wm.clone()
+        end = min(fs + pred.shape[-1], fut.shape[-1])
+        rr = min(fut.shape[1], pred.shape[-2])
+        fut[:, :rr, fs:end] = fut[:, :rr, fs:end] + pred[:, 0, :rr, :end - fs]
+        pert = vs.converter.apply_weighted_constraint(fut - wm, 0.1, 0.05, 0.08)
+        assert float(pert[..., :fs].abs().max()) == 0.0 and float(pert[..., fs:].abs().max()) > 0
+        pc = pert.cpu().numpy()
+        assert np.abs(pc[:, :24]).max() <= 0.1 + 1e-7 and np.abs(pc[:, 24:56]).max() <= 0.05 + 1e-7
+        assert np.abs(pc[:, 56:]).max() <= 0.08 + 1e-7
+        wav = vs.converter.mel_to_waveform(wm + pert)[0][:, -W:]
+        assert np.array_equal(w.chunks[k], wav.cpu().numpy()), k
