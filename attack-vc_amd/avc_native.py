@@ -39,7 +39,7 @@ class VCCfg(ctypes.Structure):
                 ("dec_c_in", ctypes.c_int32), ("dec_c_cond", ctypes.c_int32), ("dec_c_h", ctypes.c_int32),
                 ("dec_c_out", ctypes.c_int32), ("dec_kernel_size", ctypes.c_int32),
                 ("dec_n_conv_blocks", ctypes.c_int32), ("dec_upsample", ctypes.c_int32 * MAX_BLOCKS),
-                ("dec_act", ctypes.c_int32)]
+                ("dec_act", ctypes.c_int32), ("dec_sn", ctypes.c_int32)]
 
 
 class AttackOpts(ctypes.Structure):
@@ -89,6 +89,9 @@ SIGNATURES = [
     ("avc_vc_weight_count", ctypes.c_size_t, [ctypes.POINTER(VCCfg)]),
     ("avc_attach_vc", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(VCCfg), ctypes.c_void_p, ctypes.c_size_t]),
     ("avc_vc_out_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("avc_sn_state_count", ctypes.c_size_t, [ctypes.c_void_p]),
+    ("avc_set_sn_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("avc_get_sn_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("avc_content_encoder", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_content_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -157,6 +160,8 @@ SIGNATURES = [
     ("avc_profile_kernel", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_double)]),
+    ("avc_ktime", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_int64)]),
     ("avc_ws_stats", ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int64)] * 5),
     ("avc_set_ws_cache", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("avc_last_error", ctypes.c_char_p, []),
@@ -353,6 +358,30 @@ class Context:
             raise RuntimeError(f"ContentEncoder/Decoder weights: got {w.numel()} values, config needs {need}")
         _check(lib().avc_attach_vc(self.h, ctypes.byref(self._vcs), ctypes.c_void_p(w.data_ptr()), w.numel()))
 
+    _sn_dec = None
+
+    def _sn_call(self, fn):
+        """Run fn() (a call that runs Decoder forwards) with a spectral-norm Decoder's u / v loaded
+        from its module buffers and written back afterwards, as the reference's train-mode
+        spectral_norm hook updates them (models.py:382)."""
+        dec = self._sn_dec() if self._sn_dec is not None else None
+        if dec is None:
+            return fn()
+        bufs = _sn_buffers(dec)
+        uv = torch.cat([b.detach().reshape(-1).to("cpu", torch.float32) for b in bufs]).contiguous()
+        n = lib().avc_sn_state_count(self.h)
+        if uv.numel() != n:
+            raise RuntimeError(f"spectral-norm state: module holds {uv.numel()} u / v values, libavc expects {n}")
+        _check(lib().avc_set_sn_state(self.h, ctypes.c_void_p(uv.data_ptr()), n))
+        out = fn()
+        _check(lib().avc_get_sn_state(self.h, ctypes.c_void_p(uv.data_ptr()), n))
+        with torch.no_grad():
+            o = 0
+            for b in bufs:
+                b.copy_(uv[o:o + b.numel()].view_as(b))
+                o += b.numel()
+        return out
+
     def vc_out_frames(self, T: int) -> int:
         n = lib().avc_vc_out_frames(self.h, int(T))
         if n < 0:
@@ -391,8 +420,9 @@ class Context:
         out = torch.empty(B, self._vcs.dec_c_out, Tz * up, device=z.device)
         stream = torch.cuda.current_stream(z.device).cuda_stream
         with self._lock:
-            _check(lib().avc_decoder(self.h, ctypes.c_void_p(z.data_ptr()), B, Tz, ctypes.c_void_p(cond.data_ptr()),
-                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+            self._sn_call(lambda: _check(lib().avc_decoder(
+                self.h, ctypes.c_void_p(z.data_ptr()), B, Tz, ctypes.c_void_p(cond.data_ptr()),
+                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream))))
         return out
 
     def inference(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
@@ -407,7 +437,7 @@ class Context:
         out = torch.empty(B, 80, self.vc_out_frames(T), device=src.device, dtype=torch.float32)
         stream = torch.cuda.current_stream(src.device).cuda_stream
         emb = self.se_forward(tgt) if tgt.shape != src.shape else None
-        with self._lock:
+        def run():
             if emb is None:
                 _check(lib().avc_inference(self.h, ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(tgt.data_ptr()),
                                            B, T, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
@@ -415,6 +445,8 @@ class Context:
                 _check(lib().avc_inference_emb(self.h, ctypes.c_void_p(src.data_ptr()), B, T,
                                                ctypes.c_void_p(emb.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                                                ctypes.c_void_p(stream)))
+        with self._lock:
+            self._sn_call(run)
         return out
 
     def vc_attack(self, kind: str, vc_src, vc_tgt, adv_tgt, ptb0, eps: float, n_iters: int, precision="fp32",
@@ -447,7 +479,7 @@ class Context:
         else:
             same = vc_src.shape == vc_tgt.shape == adv_tgt.shape
             tgt_emb = None if same else self.se_forward(adv_tgt)
-        with self._lock:
+        def run():
             if same:
                 fn = {"e2e": lib().avc_e2e_attack, "fb": lib().avc_fb_attack}[kind]
                 _check(fn(self.h, ctypes.c_void_p(vc_src.data_ptr()), ctypes.c_void_p(vc_tgt.data_ptr()),
@@ -458,6 +490,8 @@ class Context:
                 _check(fn(self.h, ctypes.c_void_p(vc_src.data_ptr()), Ts, ctypes.c_void_p(vc_tgt.data_ptr()),
                           ctypes.c_void_p(tgt_emb.data_ptr()), ctypes.c_void_p(ptb0.data_ptr()), B, T, float(eps),
                           int(n_iters), ctypes.c_void_p(out.data_ptr()), ctypes.byref(o), ctypes.c_void_p(stream)))
+        with self._lock:
+            self._sn_call(run)
         return out, losses, grad0
 
     def ws_stats(self) -> Dict[str, int]:
@@ -477,6 +511,21 @@ class Context:
         return {v: k for k, v in ENGINE.items()}[lib().avc_get_engine(self.h, int(T))]
 
     # --- profiling (bench.py roofline) ---------------------------------------------
+    KTIME_KERNELS = ("se_fwd_fused", "se_bwd_fused", "lz_se_fwd", "lz_se_bwd", "lz_dec_fwd", "lz_dec_bwd",
+                     "dec_fwd_fused", "dec_bwd_fused")
+
+    def ktime_start(self):
+        """Start in-graph kernel timing (avc_ktime): device wall-clock stamps in the hot kernels."""
+        _check(lib().avc_ktime(self.h, 1, None, None))
+
+    def ktime_stop(self) -> Dict[str, Tuple[int, float]]:
+        """Stop in-graph kernel timing: {kernel: (launches, average launch microseconds)} for the
+        kernels that ran."""
+        us = (ctypes.c_double * 8)()
+        n = (ctypes.c_int64 * 8)()
+        _check(lib().avc_ktime(self.h, 0, us, n))
+        return {k: (int(n[i]), float(us[i])) for i, k in enumerate(self.KTIME_KERNELS) if n[i] > 0}
+
     def set_profiling(self, on: bool):
         _check(lib().avc_set_profiling(self.h, 1 if on else 0))
 
@@ -521,6 +570,7 @@ def vc_cfg_struct(ce: Dict, dec: Dict) -> VCCfg:
         setattr(s, "ce_" + k, int(ce[k]))
     for k in ("c_in", "c_cond", "c_h", "c_out", "kernel_size", "n_conv_blocks", "act"):
         setattr(s, "dec_" + k, int(dec[k]))
+    s.dec_sn = int(dec.get("sn", 0))
     sub = list(ce["subsample"])[: int(ce["n_conv_blocks"])]
     ups = list(dec["upsample"])[: int(dec["n_conv_blocks"])]
     if len(sub) > MAX_BLOCKS or len(ups) > MAX_BLOCKS:
@@ -555,7 +605,36 @@ def dec_config(dec: torch.nn.Module) -> Dict:
     return dict(c_in=dec.in_conv_layer.in_channels, c_cond=dec.conv_affine_layers[0].in_features,
                 c_h=dec.in_conv_layer.out_channels, c_out=dec.out_conv_layer.out_channels,
                 kernel_size=dec.first_conv_layers[0].kernel_size[0], n_conv_blocks=dec.n_conv_blocks,
-                upsample=list(dec.upsample), act=_act_of(dec))
+                upsample=list(dec.upsample), act=_act_of(dec), sn=int(_dec_has_sn(dec)))
+
+
+def _dec_layers(dec: torch.nn.Module):
+    """The Decoder's Conv1d / Linear layers in module (= state_dict) order (models.py:383-399)."""
+    return [dec.in_conv_layer, *dec.first_conv_layers, *dec.second_conv_layers, *dec.conv_affine_layers,
+            dec.out_conv_layer]
+
+
+def _dec_has_sn(dec: torch.nn.Module) -> bool:
+    """sn=True (models.py:382): every layer carries torch's spectral_norm (weight_orig / weight_u / weight_v)."""
+    return hasattr(dec.in_conv_layer, "weight_orig")
+
+
+def _dec_flat(dec: torch.nn.Module) -> torch.Tensor:
+    """Decoder weights for avc_attach_vc: (weight, bias) per layer in module order -- weight_orig for a
+    spectral-normed layer (libavc divides it by the layer's sigma before every Decoder forward)."""
+    parts = []
+    for m in _dec_layers(dec):
+        W = m.weight_orig if hasattr(m, "weight_orig") else m.weight
+        parts += [W.detach().reshape(-1).to("cpu", torch.float32), m.bias.detach().reshape(-1).to("cpu", torch.float32)]
+    return torch.cat(parts)
+
+
+def _sn_buffers(dec: torch.nn.Module):
+    """weight_u then weight_v of every spectral-normed Decoder layer (avc_set_sn_state's order)."""
+    out = []
+    for m in _dec_layers(dec):
+        out += [m.weight_u, m.weight_v]
+    return out
 
 
 def context_for(se: torch.nn.Module, device: torch.device) -> Context:
@@ -603,9 +682,11 @@ def vc_context_for(model: torch.nn.Module, device: torch.device) -> Context:
     version = tuple((p.data_ptr(), p._version) for m in mods for p in m.parameters())
     if getattr(ctx, "_vc_version", None) != version:
         flat = torch.cat([v.detach().reshape(-1).to("cpu", torch.float32)
-                          for m in mods for v in m.state_dict().values()])
+                          for v in model.content_encoder.state_dict().values()] + [_dec_flat(model.decoder)])
         ctx.attach_vc(ce_config(model.content_encoder), dec_config(model.decoder), flat)
         ctx._vc_version = version
+    # spectral norm: the module's weight_u / weight_v are the state every Decoder forward advances
+    ctx._sn_dec = weakref.ref(model.decoder) if _dec_has_sn(model.decoder) else None
     return ctx
 
 

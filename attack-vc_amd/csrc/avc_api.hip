@@ -18,6 +18,7 @@
 
 #include "../../include/avc.h"
 #include "avc_kernels.h"
+#include "avc_ktime.h"
 
 namespace avc {
 template <int PREC, int WM, int WN, int WGM, int WGN, int KC, int MODE, int STRIDE>
@@ -48,6 +49,8 @@ __global__ void dense_batched(DenseArgs D);
 template <int NJ>
 __global__ void dense_mfma(DenseArgs D);
 __global__ void dense_lds(DenseArgs D);
+__global__ void sn_power(SnArgs A);
+__global__ void sn_scale(SnArgs A);
 __global__ void hdr_compose(HdrArgs A);
 __global__ void hdr_update(HdrArgs A);
 __global__ void pm_conv(PmConvArgs P);
@@ -103,7 +106,7 @@ struct HostConv {
 
 enum LaunchKind {
     L_GEMM, L_HEAD, L_HEAD_V, L_FZ_FWD, L_FZ_BWD, L_DZ_FWD, L_DZ_BWD, L_DENSE, L_LZ_FWD, L_LZ_BWD, L_LZD_FWD, L_LZD_BWD,
-    L_HDR_COMPOSE, L_HDR_UPDATE
+    L_HDR_COMPOSE, L_HDR_UPDATE, L_SN_POWER, L_SN_SCALE
 };
 constexpr size_t LZ_SHMEM = 160 * 1024;   // the long kernels use the whole LDS (avc_long.hip)
 
@@ -142,6 +145,7 @@ struct Launch {
     DecArgs dz{};                // L_DZ_*: per-utterance fused Decoder pass (shape: fz_shape 0 | 8)
     DenseArgs dn{};              // L_DENSE: batched conv_affine layer (or its transpose)
     HdrArgs hd{};                // L_HDR_*: the header optimiser's elementwise ends
+    SnArgs sn{};                 // L_SN_*: spectral-norm power iteration / weight rescale
     double flop = 0;             // algorithmic FLOPs of this launch
     std::string name;
 };
@@ -263,6 +267,15 @@ static int upload(DevBuf& b, const std::vector<float>& h) {
     return 0;
 }
 
+// a table of plain structs into a float-sized device buffer
+template <class T>
+static int upload_pod(DevBuf& b, const std::vector<T>& h) {
+    static_assert(sizeof(T) % sizeof(float) == 0, "table entries are whole floats");
+    if (dalloc(b, h.size() * sizeof(T) / sizeof(float))) return 1;
+    if (!h.empty()) HIPCHK(hipMemcpy(b.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    return 0;
+}
+
 // fp32 -> bf16, round to nearest even (weights: finite values)
 static uint16_t to_bf16(float f) {
     uint32_t u;
@@ -376,7 +389,8 @@ static bool fused_cfg_ok(const avc_se_cfg& c) {
 // Fragment packing: [16-row tile][K step][lane][VE] with lane (r = l&15, q = l>>4)
 // holding A[16 mt + r][KS step + VE q + e]; zero outside [M) x [K).
 template <typename G>
-static int fz_pack(avc_ctx* ctx, int prec, int M, int K, G get, const void*& dst) {
+static int fz_pack(avc_ctx* ctx, int prec, int M, int K, G get, const void*& dst, const float** shadow = nullptr,
+                   size_t* count = nullptr) {
     const int KS = prec == PREC_F32 ? 16 : 32, VE = KS / 4;
     const int nmt = cdiv(M, 16), nst = cdiv(K, KS);
     std::vector<float> v((size_t)nmt * nst * 64 * VE, 0.f);
@@ -387,6 +401,12 @@ static int fz_pack(avc_ctx* ctx, int prec, int M, int K, G get, const void*& dst
                     const int m = 16 * mt + (l & 15), k = KS * ps + VE * (l >> 4) + e;
                     if (m < M && k < K) v[(((size_t)mt * nst + ps) * 64 + l) * VE + e] = get(m, k);
                 }
+    if (shadow) {   // the same elements in fp32, same order (spectral norm rescales from it)
+        ctx->fz_bufs.emplace_back();
+        if (upload(ctx->fz_bufs.back(), v)) return 1;
+        *shadow = ctx->fz_bufs.back().p;
+    }
+    if (count) *count = v.size();
     ctx->fz_bufs.emplace_back();
     DevBuf& b = ctx->fz_bufs.back();
     if (prec == PREC_F32) {
@@ -1582,6 +1602,12 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
     case L_HDR_COMPOSE:
         klaunch(ev, false, hdr_compose, L.grid, L.block, 0, s, L.hd);
         return hipGetLastError();
+    case L_SN_POWER:
+        klaunch(ev, false, sn_power, L.grid, L.block, 0, s, L.sn);
+        return hipGetLastError();
+    case L_SN_SCALE:
+        klaunch(ev, false, sn_scale, L.grid, L.block, 0, s, L.sn);
+        return hipGetLastError();
     case L_HDR_UPDATE:
         klaunch(ev, false, hdr_update, L.grid, L.block, 0, s, L.hd);
         return hipGetLastError();
@@ -1796,6 +1822,40 @@ extern "C" int avc_set_engine(avc_ctx* ctx, int engine) {
 extern "C" int avc_get_engine(avc_ctx* ctx, int T) {
     if (!ctx) return -1;
     return engine_for(ctx, T);
+}
+
+// In-graph kernel timing (avc_ktime.h): the records of each kernel translation unit
+extern "C" avc::KTime* avc_ktime_records_fused();
+extern "C" avc::KTime* avc_ktime_records_long();
+extern "C" avc::KTime* avc_ktime_records_vc();
+
+extern "C" int avc_ktime(avc_ctx* ctx, int enable, double* avg_us, int64_t* launches) {
+    if (!ctx) return fail("avc_ktime: null context");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    avc::KTime* units[3] = {avc_ktime_records_fused(), avc_ktime_records_long(), avc_ktime_records_vc()};
+    const int used[3] = {2, 4, 2};   // AVC_KTIME_* order: fused [0, 1], long [0..3], vc [0, 1]
+    int rate_khz = 0;
+    HIPCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, ctx->device));
+    int o = 0;
+    for (int u = 0; u < 3; ++u) {
+        if (!units[u]) return fail("avc_ktime: kernel timing records not found");
+        avc::KTime h[avc::KT_SLOTS];
+        HIPCHK(hipMemcpy(h, units[u], sizeof(h), hipMemcpyDeviceToHost));
+        for (int i = 0; i < used[u]; ++i, ++o) {
+            if (!enable) {
+                if (avg_us) avg_us[o] = h[i].n && rate_khz > 0 ? (double)h[i].sum / (double)h[i].n / rate_khz * 1e3 : 0.0;
+                if (launches) launches[o] = (int64_t)h[i].n;
+            }
+        }
+        for (int i = 0; i < avc::KT_SLOTS; ++i) {
+            h[i] = avc::KTime{};
+            h[i].on = enable ? 1ull : 0ull;
+            h[i].t0 = ~0ull;
+        }
+        HIPCHK(hipMemcpy(units[u], h, sizeof(h), hipMemcpyHostToDevice));
+    }
+    return 0;
 }
 
 extern "C" int avc_set_profiling(avc_ctx* ctx, int enable) {

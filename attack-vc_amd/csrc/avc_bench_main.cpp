@@ -124,6 +124,24 @@ int main(int argc, char** argv) {
     printf("{\"B\": %d, \"T\": %d, \"n_iters\": %d, \"steps\": %d, \"s\": %.4f, \"utts_per_s\": %.3f, "
            "\"ms_per_iter\": %.4f, \"checksum\": %.6f}\n",
            B, T, n_iters, steps, s, B * steps / s, s * 1e3 / (steps * (double)n_iters), cs);
+    // in-graph kernel durations (device wall-clock stamps, avc_ktime) over one more graph-replayed run
+    {
+        static const char* const names[8] = {"se_fwd_fused", "se_bwd_fused", "lz_se_fwd",     "lz_se_bwd",
+                                              "lz_dec_fwd",   "lz_dec_bwd",   "dec_fwd_fused", "dec_bwd_fused"};
+        double us[8];
+        int64_t nl[8];
+        CK(avc_ktime(ctx, 1, nullptr, nullptr));
+        auto k0 = std::chrono::steady_clock::now();
+        CK(run(n_iters));
+        HK(hipDeviceSynchronize());
+        const double ks = std::chrono::duration<double>(std::chrono::steady_clock::now() - k0).count();
+        CK(avc_ktime(ctx, 0, us, nl));
+        printf("{\"ktime_run_ms_per_iter\": %.4f}\n", ks * 1e3 / n_iters);
+        for (int i = 0; i < 8; ++i)
+            if (nl[i] > 0)
+                printf("{\"ktime_kernel\": \"%s\", \"launches_per_iter\": %.2f, \"avg_us\": %.3f}\n", names[i],
+                       (double)nl[i] / n_iters, us[i]);
+    }
     // per-kernel HIP-event profile of 3 iterations
     CK(avc_set_profiling(ctx, 1));
     CK(run(3));

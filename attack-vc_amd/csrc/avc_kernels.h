@@ -267,6 +267,29 @@ struct DenseArgs {
     int32_t variant;                  // DZ_VALU / DZ_MFMA / DZ_LDS (host-chosen; fixes the grid)
 };
 
+// Spectral-norm Decoder (sn=True, models.py:382: torch.nn.utils.spectral_norm, train mode since the
+// reference never calls .eval()): before every Decoder forward, sn_power runs one power iteration per
+// layer on W = weight_orig.reshape(out, -1) (v = normalize(W^T u), u = normalize(W v), sigma = u.(W v))
+// and sn_scale rewrites every packed copy of the layer's weights as weight_orig / sigma (avc_vc.hip).
+constexpr int SN_MAXDIM = 1024;   // largest out / in*k of a spectral-normed layer
+struct SnLayer {
+    int32_t h, w;                     // W is [h][w] row-major at raw + raw_off
+    int64_t raw_off, u_off, v_off;    // u [h], v [w] at uv + u_off / v_off
+};
+struct SnChunk {                      // <= SN_CHUNK elements of one packed copy of one layer
+    void* dst;                        // fp32 or bf16 (packed operand, same element order as src)
+    const float* src;                 // the same elements of weight_orig (fp32)
+    int32_t n, layer, bf16, pad;
+};
+constexpr int SN_CHUNK = 4096;
+struct SnArgs {
+    const SnLayer* layers;
+    const float* raw;
+    float* uv;
+    float* sigma;                     // [layers]
+    const SnChunk* chunks;
+};
+
 // VSMask PredictiveModel layer (avc_pm.hip): implicit GEMM over NCHW activations.
 struct PmConvArgs {
     const float* x;                   // [B][Cin][Hin][Win]

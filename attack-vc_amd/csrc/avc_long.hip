@@ -32,6 +32,8 @@
 #define AVC_FZ_RING_FREE 1   // no per-step scheduling barrier in the ring (fz_gemm_impl)
 #endif
 #include "avc_fused_core.h"
+#include "avc_ktime.h"
+AVC_KTIME_DEFINE(long)   // [0] lz_se_fwd, [1] lz_se_bwd, [2] lz_dec_fwd, [3] lz_dec_bwd (avc_ktime.h)
 
 namespace avc {
 
@@ -488,7 +490,7 @@ __device__ __forceinline__ void lz_mom_get(LzMom& M, int Tl, f32x4 (&mean)[2], f
 // forward: SpeakerEncoder (models.py:327-343) or, in ce_mode, ContentEncoder (181-210)
 // ---------------------------------------------------------------------------------
 template <int PREC>
-__global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
+__device__ __forceinline__ void lz_se_fwd_body(FusedArgs A, LongArgs L) {
     using Z = Lz<PREC>;
     constexpr int RS = Z::RS, ESZ = Z::ESZ, GRB = Z::GRB;
     constexpr int VE = 16 / ESZ, KS = 4 * VE;
@@ -862,6 +864,12 @@ __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
     FZ_PH();
     FZ_PH_DUMP("lfwd");
 }
+template <int PREC>
+__global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
+    ktime_begin(&g_ktime_long[0]);
+    lz_se_fwd_body<PREC>(A, L);
+    ktime_end(&g_ktime_long[0]);
+}
 
 // ---------------------------------------------------------------------------------
 // backward: d loss / d pooled -> conv blocks^T -> in_conv^T -> bank^T -> tanh' + Adam
@@ -875,7 +883,7 @@ struct LzBank {
 };
 
 template <int PREC>
-__global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
+__device__ __forceinline__ void lz_se_bwd_body(FusedArgs A, LongArgs L) {
     using Z = Lz<PREC>;
     using E = typename Z::E;
     constexpr int RS = Z::RS, ESZ = Z::ESZ, GRB = Z::GRB;
@@ -1266,6 +1274,12 @@ __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
     }
     FZ_PH_DUMP("lbwd");
 }
+template <int PREC>
+__global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
+    ktime_begin(&g_ktime_long[1]);
+    lz_se_bwd_body<PREC>(A, L);
+    ktime_end(&g_ktime_long[1]);
+}
 
 // ---------------------------------------------------------------------------------
 // Decoder (models.py:403-435) for any length: forward (+ e2e loss) and backward to
@@ -1316,7 +1330,7 @@ __device__ __forceinline__ void lz_ct_to_img(char* img, const float* src, int T)
 }
 
 template <int PREC>
-__global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
+__device__ __forceinline__ void lz_dec_fwd_body(DecArgs A, LongArgs L) {
     using Z = Lz<PREC>;
     constexpr int RS = Z::RS, ESZ = Z::ESZ;
     constexpr int VE = 16 / ESZ, KS = 4 * VE;
@@ -1623,9 +1637,15 @@ __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
         }
     }
 }
+template <int PREC>
+__global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
+    ktime_begin(&g_ktime_long[2]);
+    lz_dec_fwd_body<PREC>(A, L);
+    ktime_end(&g_ktime_long[2]);
+}
 
 template <int PREC>
-__global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
+__device__ __forceinline__ void lz_dec_bwd_body(DecArgs A, LongArgs L) {
     using Z = Lz<PREC>;
     constexpr int RS = Z::RS, ESZ = Z::ESZ, GRB = Z::GRB;
     constexpr int VE = 16 / ESZ, KS = 4 * VE;
@@ -1967,6 +1987,12 @@ __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
         }
         cur ^= 1;
     }
+}
+template <int PREC>
+__global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
+    ktime_begin(&g_ktime_long[3]);
+    lz_dec_bwd_body<PREC>(A, L);
+    ktime_end(&g_ktime_long[3]);
 }
 
 // LDS bytes of the long kernels (the host sets the same)

@@ -24,6 +24,8 @@
 //                   attacks, so the backward stops at the first AdaIN.
 #include "avc_fused_core.h"
 #include "avc_fused_lds.h"
+#include "avc_ktime.h"
+AVC_KTIME_DEFINE(vc)     // [0] dec_fwd_fused, [1] dec_bwd_fused (avc_ktime.h)
 
 // weight-ring depth of the standard-shape Decoder kernels: 8, with the refills pinned to their K
 // step as in avc_fused.hip (measured A/B on the e2e iteration: 0.350 -> 0.342 ms; dec_fwd_fused
@@ -128,7 +130,7 @@ __device__ __forceinline__ void zero_rows(char* img, int r0, int n, int w) {
 // forward
 // ---------------------------------------------------------------------------------
 template <int PREC, int SH>
-__global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
+__device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
     using E = typename Fz<PREC>::E;
     constexpr int RS = Fz<PREC>::RS;
     constexpr int ESZ = (int)sizeof(E);
@@ -457,12 +459,18 @@ __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
         }
     }
 }
+template <int PREC, int SH>
+__global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
+    ktime_begin(&g_ktime_vc[0]);
+    dec_fwd_fused_body<PREC, SH>(A);
+    ktime_end(&g_ktime_vc[0]);
+}
 
 // ---------------------------------------------------------------------------------
 // backward: d loss / d out -> d loss / d cond
 // ---------------------------------------------------------------------------------
 template <int PREC, int SH>
-__global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
+__device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
     using E = typename Fz<PREC>::E;
     constexpr int RS = Fz<PREC>::RS;
     constexpr int ESZ = (int)sizeof(E);
@@ -736,6 +744,12 @@ __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
         for (int l = nblk - 1; l >= 0; --l) block(IC<FZ_MAXNF>{}, l, A.Tl[l], A.up[l]);
     }
 }
+template <int PREC, int SH>
+__global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
+    ktime_begin(&g_ktime_vc[1]);
+    dec_bwd_fused_body<PREC, SH>(A);
+    ktime_end(&g_ktime_vc[1]);
+}
 
 // ---------------------------------------------------------------------------------
 // batched dense layer: Y[b][m] = sum_k A[m][k] X[b][k] (+ bias[m]); 64 rows x 32
@@ -936,6 +950,83 @@ __global__ void __launch_bounds__(256) dense_lds(DenseArgs D) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             if (m + r < D.M) Y[m + r] = y[r];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Spectral-norm Decoder (sn=True): torch.nn.utils.spectral_norm's train-mode forward pre-hook
+// (compute_weight, n_power_iterations = 1, eps 1e-12) for every layer, before each Decoder forward.
+// One workgroup per layer; fixed-order reductions (the same sigma on every run).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ float sn_block_sum(float x, float* red) {
+    red[threadIdx.x] = x;
+    __syncthreads();
+#pragma unroll
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(256) sn_power(SnArgs A) {
+#pragma clang fp contract(off)
+    __shared__ float su[SN_MAXDIM], sv[SN_MAXDIM], red[256];
+    const SnLayer L = A.layers[blockIdx.x];
+    const float* __restrict__ W = A.raw + L.raw_off;
+    float* u = A.uv + L.u_off;
+    float* v = A.uv + L.v_off;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int i = tid; i < L.h; i += 256) su[i] = u[i];
+    __syncthreads();
+    // v = normalize(W^T u): one column per thread (coalesced rows of W), rows in order
+    float ss = 0.f;
+    for (int j = tid; j < L.w; j += 256) {
+        float s = 0.f;
+        for (int i = 0; i < L.h; ++i) s = __builtin_fmaf(W[(size_t)i * L.w + j], su[i], s);
+        sv[j] = s;
+        ss = __builtin_fmaf(s, s, ss);
+    }
+    const float nv = fmaxf(sqrtf(sn_block_sum(ss, red)), 1e-12f);
+    for (int j = tid; j < L.w; j += 256) sv[j] = sv[j] / nv;
+    __syncthreads();
+    // t = W v: one row per wave, lanes over the row, then a fixed butterfly (lane 0's sum is kept)
+    for (int i = wv; i < L.h; i += 4) {
+        float s = 0.f;
+        for (int j = lane; j < L.w; j += 64) s = __builtin_fmaf(W[(size_t)i * L.w + j], sv[j], s);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+        if (lane == 0) su[i] = s;
+    }
+    __syncthreads();
+    float st = 0.f;
+    for (int i = tid; i < L.h; i += 256) st = __builtin_fmaf(su[i], su[i], st);
+    const float nt = fmaxf(sqrtf(sn_block_sum(st, red)), 1e-12f);
+    // u = normalize(t); sigma = u . (W v) = u . t
+    float sg = 0.f;
+    for (int i = tid; i < L.h; i += 256) {
+        const float ui = su[i] / nt;
+        u[i] = ui;
+        sg = __builtin_fmaf(ui, su[i], sg);
+    }
+    for (int j = tid; j < L.w; j += 256) v[j] = sv[j];
+    const float sigma = sn_block_sum(sg, red);
+    if (tid == 0) A.sigma[blockIdx.x] = sigma;
+}
+
+// every packed copy of a layer's weights <- weight_orig / sigma (torch's division), bf16 copies
+// rounded to nearest even from that fp32 quotient (the bf16 packing's conversion)
+__global__ void __launch_bounds__(256) sn_scale(SnArgs A) {
+    const SnChunk C = A.chunks[blockIdx.x];
+    const float s = A.sigma[C.layer];
+    if (C.bf16) {
+        __bf16* d = reinterpret_cast<__bf16*>(C.dst);
+        for (int i = threadIdx.x; i < C.n; i += 256) d[i] = (__bf16)(C.src[i] / s);
+    } else {
+        float* d = reinterpret_cast<float*>(C.dst);
+        for (int i = threadIdx.x; i < C.n; i += 256) d[i] = C.src[i] / s;
     }
 }
 

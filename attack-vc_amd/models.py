@@ -124,28 +124,34 @@ class SpeakerEncoder(nn.Module):
 
 
 class Decoder(_InModel, nn.Module):
-    """Parameter tree of models.py:346-401 (sn=False only); forward(z, cond)."""
+    """Parameter tree of models.py:346-401; forward(z, cond).
+
+    sn=True (models.py:382) wraps every layer in torch.nn.utils.spectral_norm exactly as the reference
+    does (same construction order, so a seeded build draws the same weights and initial u / v, and the
+    state_dict has the same weight_orig / weight_u / weight_v keys).  libavc then runs the reference's
+    train-mode arithmetic: one power iteration per Decoder forward, the weight divided by sigma, and the
+    updated u / v written back into these buffers after every call (avc_native)."""
 
     def __init__(self, c_in: int, c_cond: int, c_h: int, c_out: int, kernel_size: int,
                  n_conv_blocks: int, upsample: List[int], act: str, sn: bool, dropout_rate: float):
         super().__init__()
-        if sn:
-            raise NotImplementedError("spectral-norm Decoder (sn=True) is not supported by libavc")
+        f = nn.utils.spectral_norm if sn else (lambda m: m)
+        self.sn = bool(sn)
         self.n_conv_blocks = n_conv_blocks
         self.upsample = upsample
         self.act_name = act
-        self.in_conv_layer = nn.Conv1d(c_in, c_h, kernel_size=1)
+        self.in_conv_layer = f(nn.Conv1d(c_in, c_h, kernel_size=1))
         self.first_conv_layers = nn.ModuleList(
-            [nn.Conv1d(c_h, c_h, kernel_size=kernel_size) for _ in range(n_conv_blocks)])
+            [f(nn.Conv1d(c_h, c_h, kernel_size=kernel_size)) for _ in range(n_conv_blocks)])
         self.second_conv_layers = nn.ModuleList(
-            [nn.Conv1d(c_h, c_h * up, kernel_size=kernel_size)
+            [f(nn.Conv1d(c_h, c_h * up, kernel_size=kernel_size))
              for _, up in zip(range(n_conv_blocks), self.upsample)])
         self.norm_layer = nn.InstanceNorm1d(c_h, affine=False)
-        self.conv_affine_layers = nn.ModuleList([nn.Linear(c_cond, c_h * 2) for _ in range(n_conv_blocks * 2)])
-        self.out_conv_layer = nn.Conv1d(c_h, c_out, kernel_size=1)
+        self.conv_affine_layers = nn.ModuleList([f(nn.Linear(c_cond, c_h * 2)) for _ in range(n_conv_blocks * 2)])
+        self.out_conv_layer = f(nn.Conv1d(c_h, c_out, kernel_size=1))
         self.dropout_layer = nn.Dropout(p=dropout_rate)
         self._cfg = dict(c_in=c_in, c_cond=c_cond, c_h=c_h, c_out=c_out, kernel_size=kernel_size,
-                         n_conv_blocks=n_conv_blocks, upsample=list(upsample), act=_act_code(act))
+                         n_conv_blocks=n_conv_blocks, upsample=list(upsample), act=_act_code(act), sn=int(bool(sn)))
 
     def avc_config(self) -> Dict:
         return dict(self._cfg)

@@ -136,6 +136,7 @@ typedef struct avc_vc_cfg {
     int32_t dec_c_in, dec_c_cond, dec_c_h, dec_c_out, dec_kernel_size, dec_n_conv_blocks;
     int32_t dec_upsample[AVC_MAX_BLOCKS];
     int32_t dec_act;
+    int32_t dec_sn;    /* 1: spectral-norm Decoder (models.py:382); the weights are the weight_orig tensors */
 } avc_vc_cfg;
 
 /* Number of fp32 values avc_attach_vc expects: content_encoder.* then decoder.* parameters,
@@ -149,6 +150,22 @@ size_t avc_vc_weight_count(const avc_vc_cfg* cfg);
  * c_cond = c_h = 128, c_out = 80, odd kernel_size <= 5, <= 8 blocks, upsample 1|2; the
  * SpeakerEncoder of ctx must be fused-capable too.  Fails (non-zero) otherwise. */
 int avc_attach_vc(avc_ctx* ctx, const avc_vc_cfg* cfg, const float* weights, size_t n_weights);
+
+/* Spectral-norm Decoder (cfg->dec_sn = 1; models.py:382 wraps every Decoder layer in
+ * torch.nn.utils.spectral_norm, and the reference never calls .eval(), so each Decoder forward
+ * runs one power iteration and divides the layer's weight by sigma, updating its weight_u /
+ * weight_v buffers).  libavc does the same before every Decoder forward it runs (attacks:
+ * the precomputed targets and each iteration; inference; avc_decoder).  The state is every
+ * layer's u then v, layers in module order -- in_conv_layer, first_conv_layers.*,
+ * second_conv_layers.*, conv_affine_layers.*, out_conv_layer -- as HOST floats:
+ *   avc_sn_state_count  number of floats (0 when the attached Decoder has no spectral norm)
+ *   avc_set_sn_state    load it (before a call; the reference module's buffers)
+ *   avc_get_sn_state    read it back (after a call: the buffers' new values)
+ * Both synchronise the ctx's stream.  Replaces the weight_u / weight_v updates of
+ * torch/nn/utils/spectral_norm.py:compute_weight as the reference runs it (models.py:382). */
+size_t avc_sn_state_count(avc_ctx* ctx);
+int avc_set_sn_state(avc_ctx* ctx, const float* uv, size_t n);
+int avc_get_sn_state(avc_ctx* ctx, float* uv, size_t n);
 
 /* Frames of the Decoder output for T input frames (T -> ContentEncoder length -> x upsample). */
 int avc_vc_out_frames(avc_ctx* ctx, int T);
@@ -345,6 +362,15 @@ int avc_get_profile(avc_ctx* ctx, double* ms_per_iter, double* gemm_flop_per_ite
 int avc_profile_kernel_count(avc_ctx* ctx);
 int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len, long* launches, double* total_ms,
                        double* total_flop);
+
+/* In-graph kernel timing: the hot kernels' launch durations as they run inside the captured
+ * attack-loop graphs, with no profiler attached (each workgroup stamps the device wall clock at its
+ * start and end; a launch spans the earliest start to the latest end).  enable = 1 resets and starts
+ * recording (process-wide, on ctx's device); enable = 0 stops and writes, per kernel in the order
+ *   se_fwd_fused, se_bwd_fused, lz_se_fwd, lz_se_bwd, lz_dec_fwd, lz_dec_bwd, dec_fwd_fused, dec_bwd_fused
+ * the average launch duration in microseconds into avg_us[8] and the launch count into launches[8]
+ * (either may be NULL).  Synchronises ctx's stream. */
+int avc_ktime(avc_ctx* ctx, int enable, double* avg_us, int64_t* launches);
 
 /* Workspace cache of a context.  A context keeps the buffers, launch plans and captured hipGraphs
  * of the last few (B, T, engine) shapes it ran (6 by default; env AVC_WS_CACHE overrides), most

@@ -273,9 +273,32 @@ def instance_norm_backward(g, yhat, inv):
     return inv * (g - g.mean(axis=2, keepdims=True) - yhat * (g * yhat).mean(axis=2, keepdims=True))
 
 
+def spectral_norm_step(w, p="decoder."):
+    """sn=True (models.py:382): torch.nn.utils.spectral_norm's forward pre-hook in train mode
+    (torch/nn/utils/spectral_norm.py compute_weight; the reference never calls .eval()) for every
+    Decoder layer that has a weight_orig: one power iteration on W = weight_orig.reshape(out, -1),
+        v = normalize(W^T u),  u = normalize(W v)   (normalize: x / max(||x||, 1e-12)),
+        sigma = u . (W v),     weight = weight_orig / sigma,
+    with u, v updated in place (the module buffers weight_u / weight_v).  No-op for sn=False."""
+    for k in [k for k in w.d if k.startswith(p) and k.endswith(".weight_orig")]:
+        n = k[: -len("weight_orig")]
+        W = w.d[k]
+        Wm = W.reshape(W.shape[0], -1)
+        eps = W.dtype.type(1e-12)
+        v = Wm.T @ w.d[n + "weight_u"]
+        v = v / max(np.sqrt((v * v).sum()), eps)
+        t = Wm @ v
+        u = t / max(np.sqrt((t * t).sum()), eps)
+        w.d[n + "weight_u"], w.d[n + "weight_v"] = u, v
+        w.d[n + "weight"] = W / (u @ (Wm @ v))
+
+
 def dec_forward(w, cfg, z, cond, p="decoder.", st=None):
-    """Decoder.forward (models.py:403-435), sn=False.  st: optional list filled with
-    each block's (yhat1, z1, yhat2, z2, inv1, inv2, cond1, cond2) for dec_backward."""
+    """Decoder.forward (models.py:403-435).  st: optional list filled with each block's
+    (yhat1, z1, yhat2, z2, inv1, inv2, cond1, cond2) for dec_backward.  sn=True: every call first
+    runs spectral_norm_step (the reference's train-mode power iteration), and dec_backward then uses
+    the weights of the forward before it."""
+    spectral_norm_step(w, p)
     relu, _ = acts(cfg)
     out = relu(instance_norm(pad_conv(z, w(p + "in_conv_layer.weight"), w(p + "in_conv_layer.bias"))))
     for l in range(cfg["n_conv_blocks"]):

@@ -1,0 +1,87 @@
+"""GPU parity of the spectral-norm Decoder (sn=True, models.py:382) against the REAL reference's run
+(tests/golden/full_sn_T128.npz, tests/golden/make_sn.py): the reference never calls .eval(), so every
+Decoder forward -- the attack's precomputed targets and each iteration -- runs torch's spectral_norm
+hook in train mode (one power iteration, weight_orig / sigma, u / v updated in place).  libavc runs
+sn_power + sn_scale before each Decoder forward; the module's weight_u / weight_v buffers are loaded
+before and written back after every call (avc_native.Context._sn_call).
+
+Tolerances: the fp32 ones of tests/helpers.py (adv TOL_ADV[10], grad0 TOL_GRAD_REL_VC, loss history
+rtol 2e-4); the Decoder output 1e-4 of its max (the fused Decoder's own bound); u / v 1e-5 (fp32 power
+iteration in another summation order than torch's sgemv)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import attack_utils
+from helpers import TOL_GRAD_REL_VC, check_adv, model_from_fixture, rel
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+FN = {"e2e": attack_utils.e2e_attack, "fb": attack_utils.fb_attack}
+
+
+@pytest.fixture(scope="module")
+def sn(golden):
+    if not torch.cuda.is_available():
+        pytest.fail("no ROCm device visible")
+    z = golden("full_sn_T128")
+    m = model_from_fixture(z)          # weights and initial u / v pinned by the reference's hashes
+    assert m.decoder.sn
+    return z, m
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _uv_err(model, z, tag):
+    sd = model.decoder.state_dict()
+    return max(float(np.abs(sd[k.split("/", 1)[1]].cpu().numpy() - z[k]).max()) for k in z if k.startswith(tag + "/"))
+
+
+def test_sn_inference(sn):
+    z, m0 = sn
+    m = copy.deepcopy(m0).to(DEV)
+    assert _uv_err(m, z, "uv0") == 0.0
+    out = m.inference(_dev(z["vc_src"]), _dev(z["vc_tgt"])).cpu().numpy()
+    assert rel(out, z["inference"]) <= 1e-4, rel(out, z["inference"])
+    assert _uv_err(m, z, "uv_inference") <= 1e-5          # one power iteration, written back
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_sn_attack_golden(sn, kind):
+    """attack_utils.{e2e,fb}_attack at n = 10 on the sn=True model vs the reference's own run: adv, grad0,
+    the loss history, and the u / v left in the module (e2e: 2 precompute + 10 Decoder forwards; fb 1 + 10)."""
+    z, m0 = sn
+    m = copy.deepcopy(m0).to(DEV)
+    adv, info = FN[kind](m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
+                         ptb0=_dev(z[f"{kind}_ptb0"]), return_info=True)
+    check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10)
+    assert rel(info["grad0"].cpu().numpy(), z[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
+    np.testing.assert_allclose(info["losses"].cpu().numpy().T, z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
+    assert _uv_err(m, z, f"uv_{kind}") <= 1e-5
+
+
+@pytest.mark.parametrize("kind", ["e2e", "fb"])
+def test_sn_bf16_and_state_carries_over(sn, kind):
+    """The bench precision on the sn=True model (B = 8, n = 20): deterministic from the same u / v, the
+    objective decreases, |adv - vc| <= eps; and the state carries over between calls as in the
+    reference: a second call starts from the u / v the first left, i.e. equals the same call on a
+    model given those buffers."""
+    z, m0 = sn
+    g = torch.Generator().manual_seed(88)
+    src, vc, at, p0 = (torch.randn(8, 80, 128, generator=g).to(DEV) for _ in range(4))
+    m1, m2 = copy.deepcopy(m0).to(DEV), copy.deepcopy(m0).to(DEV)
+    a1, info = FN[kind](m1, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16", return_info=True)
+    a2 = FN[kind](m2, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16")
+    assert torch.equal(a1.detach(), a2.detach())
+    assert float((a1.detach() - vc).abs().max()) <= 0.1 + 1e-6
+    L = info["losses"].cpu().numpy()
+    assert np.all(L[-1] < L[0]), int(np.sum(L[-1] >= L[0]))
+    b1 = FN[kind](m1, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16").detach()   # from the advanced u / v
+    m3 = copy.deepcopy(m0).to(DEV)
+    m3.decoder.load_state_dict(m1.decoder.state_dict())
+    b3 = FN[kind](m3, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16").detach()
+    assert torch.equal(b1, b3)

@@ -336,3 +336,29 @@ def test_module_forwards_oracle(golden):
         y = np.where(y >= 0, y, np.float32(0.2) * y)
         assert rel(y, zm[f"pm_up{i}"]) <= 1e-5, (i, rel(y, zm[f"pm_up{i}"]))
         h = zm[f"pm_up{i}"]
+
+
+def test_spectral_norm_decoder_oracle(golden):
+    """sn=True Decoder (models.py:382; tests/golden/make_sn.py, made by the real reference): the seeded
+    build reproduces the reference's weights and initial u / v (hashes), and the oracle's train-mode
+    power iteration (oracle.spectral_norm_step, one per Decoder forward) reproduces inference, the e2e /
+    fb attacks at n = 10 (adv, grad0, losses) and the u / v the reference's buffers hold afterwards."""
+    z = golden("full_sn_T128")
+    m = model_from_fixture(z)                       # asserts the per-tensor hashes (weights, u, v)
+    assert m.decoder.sn and hasattr(m.decoder.in_conv_layer, "weight_orig")
+    sd = {k: v.detach().numpy() for k, v in m.state_dict().items()}
+    cfg = cfg_of(z)
+
+    def uv_err(w, tag):
+        return max(float(np.abs(w.d["decoder." + k.split("/", 1)[1]] - z[k]).max()) for k in z if k.startswith(tag + "/"))
+    w = oracle.Weights(sd)
+    out = oracle.inference(w, cfg, z["vc_src"], z["vc_tgt"])
+    assert rel(out, z["inference"]) <= 1e-5
+    assert uv_err(w, "uv_inference") <= 1e-6
+    for kind in ("e2e", "fb"):
+        w, rec = oracle.Weights(sd), {}
+        adv = oracle.attack(kind, w, cfg, z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 10, z[f"{kind}_ptb0"], record=rec)
+        check_adv(adv, z[f"{kind}_adv_n10"], 10)
+        assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
+        np.testing.assert_allclose(rec["losses"], z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
+        assert uv_err(w, f"uv_{kind}") <= 1e-6        # 1 (fb) / 2 (e2e) precompute forwards + 10 iterations
