@@ -1834,7 +1834,7 @@ extern "C" int avc_ktime(avc_ctx* ctx, int enable, double* avg_us, int64_t* laun
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     avc::KTime* units[3] = {avc_ktime_records_fused(), avc_ktime_records_long(), avc_ktime_records_vc()};
-    const int used[3] = {2, 4, 2};   // AVC_KTIME_* order: fused [0, 1], long [0..3], vc [0, 1]
+    const int used[3] = {4, 8, 4};   // records in use per unit (avc_ktime.h slots), in avc_ktime's output order
     int rate_khz = 0;
     HIPCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, ctx->device));
     int o = 0;

@@ -126,10 +126,10 @@ int main(int argc, char** argv) {
            B, T, n_iters, steps, s, B * steps / s, s * 1e3 / (steps * (double)n_iters), cs);
     // in-graph kernel durations (device wall-clock stamps, avc_ktime) over one more graph-replayed run
     {
-        static const char* const names[8] = {"se_fwd_fused", "se_bwd_fused", "lz_se_fwd",     "lz_se_bwd",
-                                              "lz_dec_fwd",   "lz_dec_bwd",   "dec_fwd_fused", "dec_bwd_fused"};
-        double us[8];
-        int64_t nl[8];
+        static const char* const kn[8] = {"se_fwd_fused", "se_bwd_fused", "lz_se_fwd",     "lz_se_bwd",
+                                          "lz_dec_fwd",   "lz_dec_bwd",   "dec_fwd_fused", "dec_bwd_fused"};
+        double us[16];
+        int64_t nl[16];
         CK(avc_ktime(ctx, 1, nullptr, nullptr));
         auto k0 = std::chrono::steady_clock::now();
         CK(run(n_iters));
@@ -137,10 +137,10 @@ int main(int argc, char** argv) {
         const double ks = std::chrono::duration<double>(std::chrono::steady_clock::now() - k0).count();
         CK(avc_ktime(ctx, 0, us, nl));
         printf("{\"ktime_run_ms_per_iter\": %.4f}\n", ks * 1e3 / n_iters);
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 16; ++i)
             if (nl[i] > 0)
-                printf("{\"ktime_kernel\": \"%s\", \"launches_per_iter\": %.2f, \"avg_us\": %.3f}\n", names[i],
-                       (double)nl[i] / n_iters, us[i]);
+                printf("{\"ktime_kernel\": \"%s<%s>\", \"launches_per_iter\": %.2f, \"avg_us\": %.3f}\n", kn[i / 2],
+                       (i & 1) ? "bf16" : "f32", (double)nl[i] / n_iters, us[i]);
     }
     // per-kernel HIP-event profile of 3 iterations
     CK(avc_set_profiling(ctx, 1));

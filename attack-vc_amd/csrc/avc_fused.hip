@@ -40,7 +40,7 @@
 #include "avc_ktime.h"
 #include "avc_se_head.h"
 
-AVC_KTIME_DEFINE(fused)   // [0] se_fwd_fused, [1] se_bwd_fused (avc_ktime.h)
+AVC_KTIME_DEFINE(fused)   // se_fwd_fused / se_bwd_fused, per precision (avc_ktime.h)
 
 // A-ring depth of the standard-shape kernels' 2-tile GEMMs (the generic shapes keep 4: their
 // step counts are runtime values, and the ring's end-of-GEMM rotation would not fold away)
@@ -88,8 +88,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     const int act = STD ? 0 : A.act;                   // the standard shape is ReLU (host-checked)
     FZ_PH_DECL
     FZ_PH();
-    KTime* const kt = &g_ktime_fused[0];
-    ktime_begin(kt);
+    KTime* const kt = &g_ktime_fused[KT_FUSED_FWD + (PREC == PREC_BF16)];
+    const KtStart kts = ktime_begin(kt);
     if (A.tick && b == 0 && tid == 0) atomicAdd(A.tick, 1);
 
     char* XB = fz_lds;                                  // x image [T+8][80], pad 4
@@ -396,7 +396,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
                     for (int r = 0; r < 4; ++r) mu[(size_t)(ch0 + 16 * i + r) * TN + t] = acc[i][f][r] + bi[r];
             }
         }
-        ktime_end(kt);
+        ktime_end(kt, kts);
         return;
     }
     // AdaptiveAvgPool1d(1): mean over the TN frames of each channel
@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         }
     }
     FZ_PH_DUMP("fwd");
-    ktime_end(kt);
+    ktime_end(kt, kts);
 }
 
 // ---------------------------------------------------------------------------------
@@ -461,8 +461,8 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const int ch0 = 32 * w + 4 * kq;
     FZ_PH_DECL
     FZ_PH();
-    KTime* const kt = &g_ktime_fused[1];
-    ktime_begin(kt);
+    KTime* const kt = &g_ktime_fused[KT_FUSED_BWD + (PREC == PREC_BF16)];
+    const KtStart kts = ktime_begin(kt);
     const u64* mbase = A.masks + (size_t)b * A.mask_words;
     auto mwords = [&](int layer) __attribute__((always_inline)) { return mbase + (size_t)(layer * 4 + w) * WPL; };
 
@@ -778,7 +778,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         const f32x4* R04 = reinterpret_cast<const f32x4*>(R0);
         const f32x4* R14 = reinterpret_cast<const f32x4*>(R1);
         for (int q = tid; q < FZ_CIN * T / 4; q += 256) gx[q] = R04[rq(q)] + R14[rq(q)];
-        ktime_end(kt);
+        ktime_end(kt, kts);
         return;
     }
     // Adam tail (reads ptb, m, v, vc, writes ptb, m, v, adv: 320 KB per utterance, every
@@ -842,7 +842,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     }
     FZ_PH();
     FZ_PH_DUMP("bwd");
-    ktime_end(kt);
+    ktime_end(kt, kts);
 }
 
 #define AVC_FZ_INST(P, S)                                        \

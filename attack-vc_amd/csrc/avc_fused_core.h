@@ -14,6 +14,9 @@
 #ifndef AVC_FZ_ABLATE          // timing experiments only: 1 = no A loads, 2 = no mask bookkeeping
 #define AVC_FZ_ABLATE 0
 #endif
+#ifndef AVC_FZ_LSHLOR
+#define AVC_FZ_LSHLOR 0
+#endif
 
 namespace avc {
 
@@ -482,8 +485,14 @@ struct MaskAcc {
         // re-materialises exactly that SGPR-pair compare)
         unsigned bit;
         asm("v_med3_i32 %0, %1, 0, 1" : "=v"(bit) : "v"(y));
+#if AVC_FZ_LSHLOR
+        // one v_lshl_or_b32 per bit (LLVM otherwise emits a shift per bit plus an or3 per two)
+        if (i == 0) asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(lo) : "v"(bit), "i"(4 * f + r));
+        else asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(hi) : "v"(bit), "i"(4 * f + r));
+#else
         if (i == 0) lo |= bit << (4 * f + r);
         else hi |= bit << (4 * f + r);
+#endif
     }
     __device__ __forceinline__ void store(u64* base) const {
         base[threadIdx.x & 63] = ((u64)hi << 32) | lo;
@@ -551,6 +560,16 @@ struct AdamStep {
     float nstep, bc2s, rbc2s, eps;
     float pgd;           // > 0: the opt-in sign-gradient update with this step (avc_attack_opts.update)
 };
+// the attack input of a perturbation state p (attack_utils.py:78): vc + eps * tanh(p) -- a multiply, then an
+// add, as the reference evaluates it -- or vc + p for the opt-in PGD update
+template <int PREC>
+__device__ __forceinline__ float adv_of(float x, float p, float eps, bool pgd) {
+#pragma clang fp contract(off)
+    if (pgd) return x + p;
+    if constexpr (PREC == PREC_F32) return x + eps * tanhf(p);
+    else return __builtin_fmaf(eps, fast_tanh(p), x);
+}
+
 template <int PREC>
 __device__ __forceinline__ void adam_elem(const AdamArgs& Ad, const AdamStep& S, float gsum, float x, float& p,
                                           float& mm, float& vv, float& g, float& ad) {
@@ -563,7 +582,7 @@ __device__ __forceinline__ void adam_elem(const AdamArgs& Ad, const AdamStep& S,
         g = gsum;
         const float sg = gsum > 0.f ? 1.f : (gsum < 0.f ? -1.f : 0.f);
         p = fminf(fmaxf(p - S.pgd * sg, -S.eps), S.eps);
-        ad = x + p;
+        ad = adv_of<PREC>(x, p, S.eps, true);
         return;
     }
     if constexpr (PREC == PREC_F32) {
@@ -573,7 +592,7 @@ __device__ __forceinline__ void adam_elem(const AdamArgs& Ad, const AdamStep& S,
         vv = vv * Ad.b2;
         vv = vv + Ad.b2c * g * g;
         p = p + S.nstep * (mm / (sqrtf(vv) / S.bc2s + Ad.adam_eps));
-        ad = x + S.eps * tanhf(p);
+        ad = adv_of<PREC>(x, p, S.eps, false);
     } else {
         const float th = fast_tanh(p);
         g = (gsum * S.eps) * __builtin_fmaf(-th, th, 1.f);
@@ -581,7 +600,7 @@ __device__ __forceinline__ void adam_elem(const AdamArgs& Ad, const AdamStep& S,
         vv = __builtin_fmaf(Ad.b2c * g, g, vv * Ad.b2);
         const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(vv), S.rbc2s, Ad.adam_eps);
         p = __builtin_fmaf(S.nstep, mm * __builtin_amdgcn_rcpf(den), p);
-        ad = __builtin_fmaf(S.eps, fast_tanh(p), x);
+        ad = adv_of<PREC>(x, p, S.eps, false);
     }
 }
 

@@ -661,6 +661,9 @@ __global__ void __launch_bounds__(256) hdr_update(HdrArgs A) {
 // pgd: the sign-gradient mode keeps delta = eps*tanh(ptb0) itself (the same starting adv)
 __global__ void attack_init(const float* __restrict__ vc, const float* __restrict__ ptb0, float* ptb, float* m,
                             float* v, float* adv, float eps, size_t n, int pgd) {
+    // vc + eps * tanh(ptb) as the reference evaluates it (a multiply, then an add: no fma), like the
+    // Adam tail and the forward's adv (adv_of, avc_fused_core.h)
+#pragma clang fp contract(off)
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float p = ptb0[i];

@@ -33,7 +33,7 @@
 #endif
 #include "avc_fused_core.h"
 #include "avc_ktime.h"
-AVC_KTIME_DEFINE(long)   // [0] lz_se_fwd, [1] lz_se_bwd, [2] lz_dec_fwd, [3] lz_dec_bwd (avc_ktime.h)
+AVC_KTIME_DEFINE(long)   // lz_se_fwd, lz_se_bwd, lz_dec_fwd, lz_dec_bwd per precision (avc_ktime.h)
 
 namespace avc {
 
@@ -866,9 +866,9 @@ __device__ __forceinline__ void lz_se_fwd_body(FusedArgs A, LongArgs L) {
 }
 template <int PREC>
 __global__ void __launch_bounds__(256, 1) lz_se_fwd(FusedArgs A, LongArgs L) {
-    ktime_begin(&g_ktime_long[0]);
+    const KtStart kts = ktime_begin(&g_ktime_long[KT_LZ_SE_FWD + (PREC == PREC_BF16)]);
     lz_se_fwd_body<PREC>(A, L);
-    ktime_end(&g_ktime_long[0]);
+    ktime_end(&g_ktime_long[KT_LZ_SE_FWD + (PREC == PREC_BF16)], kts);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1276,9 +1276,9 @@ __device__ __forceinline__ void lz_se_bwd_body(FusedArgs A, LongArgs L) {
 }
 template <int PREC>
 __global__ void __launch_bounds__(256, 1) lz_se_bwd(FusedArgs A, LongArgs L) {
-    ktime_begin(&g_ktime_long[1]);
+    const KtStart kts = ktime_begin(&g_ktime_long[KT_LZ_SE_BWD + (PREC == PREC_BF16)]);
     lz_se_bwd_body<PREC>(A, L);
-    ktime_end(&g_ktime_long[1]);
+    ktime_end(&g_ktime_long[KT_LZ_SE_BWD + (PREC == PREC_BF16)], kts);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1639,9 +1639,9 @@ __device__ __forceinline__ void lz_dec_fwd_body(DecArgs A, LongArgs L) {
 }
 template <int PREC>
 __global__ void __launch_bounds__(256, 1) lz_dec_fwd(DecArgs A, LongArgs L) {
-    ktime_begin(&g_ktime_long[2]);
+    const KtStart kts = ktime_begin(&g_ktime_long[KT_LZ_DEC_FWD + (PREC == PREC_BF16)]);
     lz_dec_fwd_body<PREC>(A, L);
-    ktime_end(&g_ktime_long[2]);
+    ktime_end(&g_ktime_long[KT_LZ_DEC_FWD + (PREC == PREC_BF16)], kts);
 }
 
 template <int PREC>
@@ -1990,9 +1990,9 @@ __device__ __forceinline__ void lz_dec_bwd_body(DecArgs A, LongArgs L) {
 }
 template <int PREC>
 __global__ void __launch_bounds__(256, 1) lz_dec_bwd(DecArgs A, LongArgs L) {
-    ktime_begin(&g_ktime_long[3]);
+    const KtStart kts = ktime_begin(&g_ktime_long[KT_LZ_DEC_BWD + (PREC == PREC_BF16)]);
     lz_dec_bwd_body<PREC>(A, L);
-    ktime_end(&g_ktime_long[3]);
+    ktime_end(&g_ktime_long[KT_LZ_DEC_BWD + (PREC == PREC_BF16)], kts);
 }
 
 // LDS bytes of the long kernels (the host sets the same)

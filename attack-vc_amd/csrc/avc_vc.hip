@@ -25,7 +25,7 @@
 #include "avc_fused_core.h"
 #include "avc_fused_lds.h"
 #include "avc_ktime.h"
-AVC_KTIME_DEFINE(vc)     // [0] dec_fwd_fused, [1] dec_bwd_fused (avc_ktime.h)
+AVC_KTIME_DEFINE(vc)     // dec_fwd_fused, dec_bwd_fused per precision (avc_ktime.h)
 
 // weight-ring depth of the standard-shape Decoder kernels: 8, with the refills pinned to their K
 // step as in avc_fused.hip (measured A/B on the e2e iteration: 0.350 -> 0.342 ms; dec_fwd_fused
@@ -461,9 +461,9 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
 }
 template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
-    ktime_begin(&g_ktime_vc[0]);
+    const KtStart kts = ktime_begin(&g_ktime_vc[KT_DEC_FWD + (PREC == PREC_BF16)]);
     dec_fwd_fused_body<PREC, SH>(A);
-    ktime_end(&g_ktime_vc[0]);
+    ktime_end(&g_ktime_vc[KT_DEC_FWD + (PREC == PREC_BF16)], kts);
 }
 
 // ---------------------------------------------------------------------------------
@@ -746,9 +746,9 @@ __device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
 }
 template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
-    ktime_begin(&g_ktime_vc[1]);
+    const KtStart kts = ktime_begin(&g_ktime_vc[KT_DEC_BWD + (PREC == PREC_BF16)]);
     dec_bwd_fused_body<PREC, SH>(A);
-    ktime_end(&g_ktime_vc[1]);
+    ktime_end(&g_ktime_vc[KT_DEC_BWD + (PREC == PREC_BF16)], kts);
 }
 
 // ---------------------------------------------------------------------------------

@@ -555,7 +555,7 @@ def main():
         else:
             ctx.vc_attack(a.attack, src, vc, at, p0, a.eps, KTIME_ITERS, precision=a.precision)
         kt = ctx.ktime_stop()
-        eager = {k.split("<")[0]: (k, v) for k, v in stats.items()}
+        eager = {k: (k, v) for k, v in stats.items()}
         timed = {k: v for k, v in kt.items() if k in eager}
         peak, unit = PEAK[a.precision]
         if timed:   # dominant kernel by in-graph time per iteration

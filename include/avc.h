@@ -366,10 +366,10 @@ int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len, long* laun
 /* In-graph kernel timing: the hot kernels' launch durations as they run inside the captured
  * attack-loop graphs, with no profiler attached (each workgroup stamps the device wall clock at its
  * start and end; a launch spans the earliest start to the latest end).  enable = 1 resets and starts
- * recording (process-wide, on ctx's device); enable = 0 stops and writes, per kernel in the order
- *   se_fwd_fused, se_bwd_fused, lz_se_fwd, lz_se_bwd, lz_dec_fwd, lz_dec_bwd, dec_fwd_fused, dec_bwd_fused
- * the average launch duration in microseconds into avg_us[8] and the launch count into launches[8]
- * (either may be NULL).  Synchronises ctx's stream. */
+ * recording (process-wide, on ctx's device); enable = 0 stops and writes, per kernel and precision in
+ * the order se_fwd_fused, se_bwd_fused, lz_se_fwd, lz_se_bwd, lz_dec_fwd, lz_dec_bwd, dec_fwd_fused,
+ * dec_bwd_fused, each as <fp32> then <bf16>, the average launch duration in microseconds into avg_us[16]
+ * and the launch count into launches[16] (either may be NULL).  Synchronises ctx's stream. */
 int avc_ktime(avc_ctx* ctx, int enable, double* avg_us, int64_t* launches);
 
 /* Workspace cache of a context.  A context keeps the buffers, launch plans and captured hipGraphs

@@ -38,8 +38,13 @@ TOL_VC_GRAD_L2_MEDIAN = 2e-5
 # bounds are ~3x the largest distance any GPU test measured (AVC_TOL_LOG, profiles/r04/tol_log.json):
 # max 2.4e-7 / 1.6e-5 / 3.3e-5 / 6.1e-5 and mean 2.3e-9 / 8.9e-8 / 2.1e-7 / 1.4e-6 at n = 1 / 10 / 100 /
 # 1500; SURVEY 8(c)'s n = 100 / 1500 bounds are met with room (1e-4; 5e-3, mean 1e-4).
+# Round 5: the mean bound at n = 10 is 2e-7.  The fb chain through the Decoder is the worst case: on
+# full_lrelu_T128 the reference's OWN fp32 run is 9.3e-8 (mean) from its float64 evaluation (numpy oracle in
+# float64 vs the golden; 5.5e-8 for the oracle's fp32), so an independent fp32 evaluation can sit ~2x that
+# from the golden (measured 1.37e-7 once every engine computes vc + eps * tanh(ptb) unfused, as the
+# reference does).
 TOL_ADV = {1: 1e-6, 10: 5e-5, 100: 1e-4, 1500: 5e-4}
-TOL_ADV_MEAN = {1: 1e-8, 10: 1e-7, 100: 1e-6, 1500: 5e-6}
+TOL_ADV_MEAN = {1: 1e-8, 10: 2e-7, 100: 1e-6, 1500: 5e-6}
 
 
 def check_grad_flip_robust(g, ref, frac=0.05):
@@ -107,26 +112,76 @@ def rel(a, b):
 
 def oracle_grad0_instrumented(kind, w, cfg, src, vc, at, p0, flip=None):
     """The oracle's iteration-0 gradient of a `kind` attack (float64 weights/inputs for the
-    calibration tests) with every ReLU call numbered in call order.  Returns (grad0, pre): pre[i]
-    is call i's pre-activation.  flip=(i, idx) inverts call i's ReLU mask at element idx (forward
-    and backward: the oracle's act' reads the post-activation), i.e. the other branch of a unit
-    whose pre-activation is within rounding of zero.  Test infrastructure for
-    test_gpu_vc_full.py::test_fb_grad0_drift_is_one_relu_flip."""
+    calibration tests) with every activation call numbered in call order.  Returns (grad0, pre):
+    pre[i] is call i's pre-activation.  flip=(i, idx) makes call i's unit idx take the other branch
+    of its (Leaky)ReLU -- a pre-activation within rounding of zero evaluated with the other sign: its
+    output gets the other sign (the oracle's act' reads the sign of the output, so the backward
+    follows); a list of such pairs flips several units.  Test infrastructure for the fb iteration-0
+    localisation tests."""
     pre = []
-
-    def relu(x):
-        i = len(pre)
-        pre.append(x)
-        m = x > 0
-        if flip is not None and flip[0] == i:
-            m = m.copy()
-            m[flip[1]] = ~m[flip[1]]
-        return np.where(m, x, 0)
     orig = oracle.acts
-    oracle.acts = lambda c: (relu, (lambda y: (y > 0).astype(y.dtype)))
+    flips = [] if flip is None else ([flip] if isinstance(flip[0], int) else list(flip))
+
+    def acts(c):
+        act, dact = orig(c)
+
+        def a(x):
+            i = len(pre)
+            pre.append(x)
+            y = act(x)
+            for fi, j in flips:
+                if fi == i:
+                    y = y.copy()
+                    y[j] = act(-x[j]) if x[j] > 0 else -x[j]
+            return y
+        return a, dact
+    oracle.acts = acts
     try:
         rec = {}
         oracle.attack(kind, w, cfg, src, vc, at, 0.1, 1, p0, record=rec)
     finally:
         oracle.acts = orig
     return rec["grad0"], pre
+
+
+def vc_grad0_explained(kind, model, cfg, ins, g_gpu, rel_ok=1e-5, tol=5e-6, ref64=None):
+    """The e2e / fb iteration-0 gradient of ONE utterance (ins: its vc_src, vc_tgt, adv_tgt, ptb0 [1, 80, T])
+    vs the reference's arithmetic in float64: within rel_ok of max |g|, or -- the fb / e2e chain funnels a
+    Decoder / feedback-encoder unit that takes the other (Leaky)ReLU branch through the 128-wide embedding
+    gradients, moving every element of the utterance -- within `tol` of the float64 gradient with one (or two)
+    units of the attack iteration's forward flipped, units whose pre-activation is within 1e-6 of its layer's
+    max.  Returns (ok, report)."""
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    w64 = oracle.Weights(sd, dtype=np.float64)
+    f64 = [np.asarray(t, np.float64) for t in ins]
+    g64, pre = oracle_grad0_instrumented(kind, w64, cfg, *f64)
+    if ref64 is not None:
+        assert np.abs(g64 - ref64).max() <= 1e-12 * np.abs(ref64).max()
+    gmax = np.abs(g64).max()
+    g = np.asarray(g_gpu, np.float64).reshape(g64.shape)
+    e0 = float(np.abs(g - g64).max() / gmax)
+    if e0 <= rel_ok:
+        return True, f"within {e0:.2e} of float64"
+    se = cfg["SpeakerEncoder"]
+    n_se = len(range(se["bank_scale"], se["bank_size"] + 1, se["bank_scale"])) + 1 + 2 * se["n_conv_blocks"] + \
+        2 * se["n_dense_blocks"]
+    n_it = n_se + 1 + 2 * cfg["Decoder"]["n_conv_blocks"] + (n_se if kind == "fb" else 0)
+    first = len(pre) - n_it
+    cand = []
+    for i in range(first, len(pre)):
+        r = np.abs(pre[i]) / np.abs(pre[i]).max()
+        j = np.unravel_index(np.argmin(r), r.shape)
+        if r[j] < 1e-6:
+            cand.append((float(r[j]), i, j))
+    best, rep = None, [f"float64 {e0:.2e}"]
+    cand = sorted(cand)
+    sets = [[c] for c in cand] + [[a, b] for k, a in enumerate(cand) for b in cand[k + 1:]]   # one flip, then two
+    for fs in sets:
+        gf, _ = oracle_grad0_instrumented(kind, w64, cfg, *f64, flip=[(i, j) for _, i, j in fs])
+        e = float(np.abs(g - gf).max() / gmax)
+        rep.append("flip " + " + ".join(f"call {i - first} {tuple(int(v) for v in j)} (|pre| {r:.1e})" for r, i, j in fs) +
+                   f": {e:.2e}")
+        best = e if best is None else min(best, e)
+        if e <= tol:
+            break
+    return best is not None and best <= tol, "; ".join(rep)

@@ -1,6 +1,8 @@
 """GPU parity of the LeakyReLU AdaIN-VC variant (act="lrelu", models.py:107-118) against
 the reference's outputs (tests/golden/full_lrelu_T128.npz): the fused kernels' generic
 shapes with a runtime activation (the standard shape is compiled for ReLU only)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -43,7 +45,20 @@ def test_lrelu_attacks(lrelu, kind):
         fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
         adv, info = fn(m, t["vc_src"], t["vc_tgt"], t["adv_tgt"], 0.1, 10, ptb0=t[f"{kind}_ptb0"], return_info=True)
     check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10)
-    assert rel(info["grad0"].cpu().numpy(), z[f"{kind}_grad0"]) <= (TOL_GRAD_REL_VC if kind != "emb" else TOL_GRAD_REL)
+    g = info["grad0"].cpu().numpy()
+    if kind == "emb":
+        assert rel(g, z[f"{kind}_grad0"]) <= TOL_GRAD_REL
+    elif rel(g, z[f"{kind}_grad0"]) > TOL_GRAD_REL_VC:
+        # the e2e / fb iteration-0 gradient is ill-conditioned at isolated units: the distance must be one
+        # LeakyReLU unit within rounding of zero taking the other slope (helpers.vc_grad0_explained)
+        from helpers import cfg_of, vc_grad0_explained
+        for u in range(g.shape[0]):
+            ok, rep = vc_grad0_explained(kind, m, cfg_of(z), [z[k][u:u + 1] for k in ("vc_src", "vc_tgt", "adv_tgt",
+                                                                                    f"{kind}_ptb0")], g[u:u + 1])
+            print(f"utterance {u}: {rep}")
+            if not ok and os.path.isdir("gpurun_out"):
+                np.save(f"gpurun_out/lrelu_{kind}_grad0.npy", g)
+            assert ok, (u, rep)
 
 
 @pytest.mark.parametrize("T", [300, 200])

@@ -66,22 +66,28 @@ def test_sn_attack_golden(sn, kind):
 
 @pytest.mark.parametrize("kind", ["e2e", "fb"])
 def test_sn_bf16_and_state_carries_over(sn, kind):
-    """The bench precision on the sn=True model (B = 8, n = 20): deterministic from the same u / v, the
-    objective decreases, |adv - vc| <= eps; and the state carries over between calls as in the
-    reference: a second call starts from the u / v the first left, i.e. equals the same call on a
-    model given those buffers."""
+    """The bench precision on the sn=True model (B = 8, n = 20): deterministic from the same u / v,
+    |adv - vc| <= eps, within SURVEY 8(c)'s bf16 bound (2e-2) of the fp32 attack from the same state, and
+    the state carries over between calls as in the reference: a second call starts from the u / v the
+    first left, i.e. equals the same call on a model given those buffers.  (No loss-decrease check: the
+    power iteration changes the Decoder every forward, so the objective moves under the attack -- the
+    reference's own fp32 e2e loss rises from -2.2e-3 to 5.6e-3 over 10 iterations in full_sn_T128.npz.)"""
     z, m0 = sn
     g = torch.Generator().manual_seed(88)
     src, vc, at, p0 = (torch.randn(8, 80, 128, generator=g).to(DEV) for _ in range(4))
-    m1, m2 = copy.deepcopy(m0).to(DEV), copy.deepcopy(m0).to(DEV)
-    a1, info = FN[kind](m1, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16", return_info=True)
-    a2 = FN[kind](m2, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16")
-    assert torch.equal(a1.detach(), a2.detach())
-    assert float((a1.detach() - vc).abs().max()) <= 0.1 + 1e-6
-    L = info["losses"].cpu().numpy()
-    assert np.all(L[-1] < L[0]), int(np.sum(L[-1] >= L[0]))
+    m1, m2, m4 = (copy.deepcopy(m0).to(DEV) for _ in range(3))
+    a1 = FN[kind](m1, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16").detach()
+    a2 = FN[kind](m2, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16").detach()
+    a4 = FN[kind](m4, src, vc, at, 0.1, 20, ptb0=p0).detach()
+    assert torch.equal(a1, a2)
+    assert float((a1 - vc).abs().max()) <= 0.1 + 1e-6
+    assert float((a1 - a4).abs().max()) <= 2e-2, float((a1 - a4).abs().max())
+    assert _uv_err(m1, z, "uv0") > 0                      # the buffers moved
+    state = {k: v.clone() for k, v in m1.decoder.state_dict().items()}
     b1 = FN[kind](m1, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16").detach()   # from the advanced u / v
     m3 = copy.deepcopy(m0).to(DEV)
-    m3.decoder.load_state_dict(m1.decoder.state_dict())
+    m3.decoder.load_state_dict(state)
     b3 = FN[kind](m3, src, vc, at, 0.1, 20, ptb0=p0, precision="bf16").detach()
-    assert torch.equal(b1, b3)
+    assert torch.equal(b1, b3), float((b1 - b3).abs().max())
+    for k, v in m3.decoder.state_dict().items():          # and both leave the same u / v
+        assert torch.equal(v, m1.decoder.state_dict()[k]), k
