@@ -125,7 +125,10 @@ int main(int argc, char** argv) {
            "\"ms_per_iter\": %.4f, \"checksum\": %.6f}\n",
            B, T, n_iters, steps, s, B * steps / s, s * 1e3 / (steps * (double)n_iters), cs);
     // in-graph kernel durations (device wall-clock stamps, avc_ktime) over one more graph-replayed run
-    {
+    // (AVC_BENCH_KTIME=0 skips it: a rocprofv3 kernel trace then averages the timed run's launches only --
+    // the recording run's launches end with a serialised atomic tail)
+    const char* kte = getenv("AVC_BENCH_KTIME");
+    if (!(kte && kte[0] == '0')) {
         static const char* const kn[8] = {"se_fwd_fused", "se_bwd_fused", "lz_se_fwd",     "lz_se_bwd",
                                           "lz_dec_fwd",   "lz_dec_bwd",   "dec_fwd_fused", "dec_bwd_fused"};
         double us[16];

@@ -121,6 +121,19 @@ __device__ __forceinline__ void fft_lds(float2* Z, const float2* TW) {
     }
 }
 
+// sum over the 16 lanes of a row, every lane receiving it (DPP: rotate 8, 4 in the row, quad swaps 2, 1)
+template <int CTRL>
+__device__ __forceinline__ float dsp_dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dsp_row16_sum(float v) {
+    v += dsp_dpp<0x128>(v);
+    v += dsp_dpp<0x124>(v);
+    v += dsp_dpp<0x4E>(v);
+    v += dsp_dpp<0xB1>(v);
+    return v;
+}
+
 // numpy.pad(mode='reflect') index into [0, L) (no edge repeat; any overhang), or -1 (constant)
 __device__ __forceinline__ int pad_index(int s, int L, int pad_mode) {
     if (s >= 0 && s < L) return s;
@@ -180,13 +193,19 @@ __global__ void __launch_bounds__(DSP_THREADS) dsp_wav2mel(DspArgs A) {
         MAG[F + k] = A.flavor ? p1 : sqrtf(p1);
     }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < 2 * A.n_mels; idx += DSP_THREADS) {
+    // one (frame, mel) dot product per 16-lane row: lane l sums the filter's bins f = lo + l, lo + l + 16, ..
+    // (coalesced reads of the filter row and of MAG), then a fixed-order DPP reduction over the row --
+    // round 4 ran each dot product serially in one thread (up to ~60 dependent L2 loads for the top mels:
+    // the kernel's critical path)
+    const int l16 = threadIdx.x & 15;
+    for (int idx = threadIdx.x >> 4; idx < 2 * A.n_mels; idx += DSP_THREADS / 16) {
         const int fr = idx / A.n_mels, m = idx - fr * A.n_mels, t = t0 + fr;
-        if (t >= Tf) continue;
         const float* row = A.mel_basis + (size_t)m * F;
         const float* mg = MAG + fr * F;
         float s = 0.f;
-        for (int f = A.mel_range[2 * m]; f < A.mel_range[2 * m + 1]; ++f) s = fmaf(row[f], mg[f], s);
+        for (int f = A.mel_range[2 * m] + l16; f < A.mel_range[2 * m + 1]; f += 16) s = fmaf(row[f], mg[f], s);
+        s = dsp_row16_sum(s);
+        if (t >= Tf || l16 != 0) continue;
         float v;
         if (A.flavor) {
             v = log10f(fmaxf(s, 1e-5f));                   // log10(clamp(mel, 1e-5)) (utils/audio.py:55-56)

@@ -47,6 +47,15 @@ AVC_KTIME_DEFINE(fused)   // se_fwd_fused / se_bwd_fused, per precision (avc_kti
 #ifndef AVC_FZ_RD_FWD
 #define AVC_FZ_RD_FWD 8
 #endif
+// round-5 epilogue VALU cuts (A/B on the emb iteration, bit-identical results): the stride-2 pool from
+// DPP pair sums (2 lane shuffles per element instead of 4) and the bank / conv1 ReLU on packed bf16 pairs
+// -- 0.1768 -> 0.1756 ms together
+#ifndef AVC_FZ_POOLDPP
+#define AVC_FZ_POOLDPP 1
+#endif
+#ifndef AVC_FZ_PKRELU
+#define AVC_FZ_PKRELU 1
+#endif
 #ifndef AVC_FZ_RD_BWD
 #define AVC_FZ_RD_BWD 8
 #endif
@@ -76,6 +85,8 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     constexpr int VE = 16 / ESZ, KS = 4 * VE;
     constexpr int NF = 8;
     constexpr bool DBUF = PREC == PREC_BF16;   // double-buffered bank output (LDS room)
+    // bf16, standard shape (ReLU, no ContentEncoder InstanceNorm there): bank / conv1 epilogues pack first
+    constexpr bool PKRELU = AVC_FZ_PKRELU && PREC == PREC_BF16 && STD != 0;
     const int b = blockIdx.x;
     const int T = STD ? StdSE::T : A.T;
     const int nb = STD ? StdSE::NB : A.nb;
@@ -191,14 +202,21 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 if (f >= nf0) continue;
-                f32x4 y;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    y[r] = act_f(acc[i][f][r] + bi[r], act);
-                    mk.put(i, f, r, y[r]);
-                }
                 const int t = 16 * f + c;
-                if (t < T) st4<PREC>(BK + t * RS + (ch0 + 16 * i) * ESZ, y);
+                if constexpr (PKRELU) {   // ReLU' bit from the pre-activation, ReLU on the packed bf16 pairs
+                    const f32x4 x = acc[i][f] + bi;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) mk.put(i, f, r, x[r]);
+                    if (t < T) *reinterpret_cast<u32x2*>(BK + t * RS + (ch0 + 16 * i) * ESZ) = relu_pk_bf16x4(x);
+                } else {
+                    f32x4 y;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        y[r] = act_f(acc[i][f][r] + bi[r], act);
+                        mk.put(i, f, r, y[r]);
+                    }
+                    if (t < T) st4<PREC>(BK + t * RS + (ch0 + 16 * i) * ESZ, y);
+                }
             }
         }
         if (wm) mk.store(mbase + (size_t)(kb * 4 + w) * WPL);
@@ -287,14 +305,20 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 if (f >= nfi) continue;
-                f32x4 y;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    y[r] = act_f(acc[i][f][r], act);
-                    mk.put(i, f, r, y[r]);
-                }
                 const int t = 16 * f + c;
-                if (t < Ti) put_reflect<PREC>(YB, t, Ti, P, (ch0 + 16 * i) * ESZ, y);
+                if constexpr (PKRELU) {   // as in the bank epilogue (the conv1 output only feeds conv2's image)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) mk.put(i, f, r, acc[i][f][r]);
+                    if (t < Ti) put_reflect_pk(YB, t, Ti, P, (ch0 + 16 * i) * ESZ, relu_pk_bf16x4(acc[i][f]));
+                } else {
+                    f32x4 y;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        y[r] = act_f(acc[i][f][r], act);
+                        mk.put(i, f, r, y[r]);
+                    }
+                    if (t < Ti) put_reflect<PREC>(YB, t, Ti, P, (ch0 + 16 * i) * ESZ, y);
+                }
             }
         }
         if (wm) mk.store(mbase + (size_t)((nb + 1 + 2 * l) * 4 + w) * WPL);
@@ -307,7 +331,30 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfo, ring, op_c2(l),
                                       l + 1 < nblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l)), YB, rb);
         FZ_PH();
-        if (s == 2) {
+        if (AVC_FZ_POOLDPP && STD != 0 && s == 2) {
+            // the standard shape's stride-2 layers have even input lengths: every pooled frame averages a
+            // pair.  The pair sum h[2t'] + h[2t'+1] is formed in place by a quad-permute DPP add (lane 2k
+            // holds it; the same bits as the add below, fp addition being commutative), then one lane
+            // shuffle per source fragment compacts it -- 2 ds_bpermute per element instead of 4.
+            const int src0 = (lane & 48) | ((2 * c) & 15);
+#pragma unroll
+            for (int fo = 0; fo < NF; ++fo) {
+                if (fo >= nfo) continue;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const f32x4 sa = hres[i][(2 * fo) < NF ? 2 * fo : NF - 1];
+                    const f32x4 sb = hres[i][(2 * fo + 1) < NF ? 2 * fo + 1 : NF - 1];
+                    f32x4 pv;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float pa = sa[r] + dpp_mov<0xB1>(sa[r]), pb = sb[r] + dpp_mov<0xB1>(sb[r]);
+                        const float a = __shfl(pa, src0), bb = __shfl(pb, src0);
+                        pv[r] = (c < 8 ? a : bb) / 2.f;
+                    }
+                    hres[i][fo] = pv;
+                }
+            }
+        } else if (s == 2) {
             // pooled[t'] = (h[2t'] + h[2t'+1]) / cnt : sources in frags 2f', 2f'+1; increasing f'
             // order keeps the in-place update safe (frag f' is read before it is written)
             const int src0 = (lane & 48) | ((2 * c) & 15), src1 = (lane & 48) | ((2 * c + 1) & 15);

@@ -14,9 +14,6 @@
 #ifndef AVC_FZ_ABLATE          // timing experiments only: 1 = no A loads, 2 = no mask bookkeeping
 #define AVC_FZ_ABLATE 0
 #endif
-#ifndef AVC_FZ_LSHLOR
-#define AVC_FZ_LSHLOR 0
-#endif
 
 namespace avc {
 
@@ -65,6 +62,26 @@ __device__ __forceinline__ void st4(char* p, f32x4 v) {
     } else {
         *reinterpret_cast<u32x2*>(p) = pk_bf16x4(v);
     }
+}
+
+// ReLU on two packed bf16 values (v_pk_max_i16 against 0: a negative bf16 is a negative int16, -0 becomes
+// +0): bf16(relu(x)) == relu(bf16(x)) bit for bit, so an epilogue whose output only feeds an operand
+// image (no fp32 copy kept) packs first and applies the ReLU to pairs -- half the instructions
+__device__ __forceinline__ unsigned relu_pk_bf16(unsigned v) {
+    unsigned r;
+    asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(v));
+    return r;
+}
+__device__ __forceinline__ u32x2 relu_pk_bf16x4(const f32x4& x) {
+    const u32x2 p = pk_bf16x4(x);
+    return u32x2{relu_pk_bf16(p[0]), relu_pk_bf16(p[1])};
+}
+// write 4 packed bf16 channels of frame t of a padded operand image (pad P rows each side, reflect)
+__device__ __forceinline__ void put_reflect_pk(char* img, int t, int T, int P, int chbyte, u32x2 v) {
+    constexpr int RS = 288;
+    *reinterpret_cast<u32x2*>(img + (P + t) * RS + chbyte) = v;
+    if (t >= 1 && t <= P) *reinterpret_cast<u32x2*>(img + (P - t) * RS + chbyte) = v;
+    if (t >= T - 1 - P && t <= T - 2) *reinterpret_cast<u32x2*>(img + (P + 2 * T - 2 - t) * RS + chbyte) = v;
 }
 
 template <int PREC>
@@ -485,14 +502,10 @@ struct MaskAcc {
         // re-materialises exactly that SGPR-pair compare)
         unsigned bit;
         asm("v_med3_i32 %0, %1, 0, 1" : "=v"(bit) : "v"(y));
-#if AVC_FZ_LSHLOR
-        // one v_lshl_or_b32 per bit (LLVM otherwise emits a shift per bit plus an or3 per two)
+        // one v_lshl_or_b32 per bit: LLVM otherwise emits a shift per bit plus a v_or3 per two (1.5 VALU
+        // per bit; an epilogue sets 64) -- measured 0.1782 -> 0.1766 ms per emb iteration (A/B, round 5)
         if (i == 0) asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(lo) : "v"(bit), "i"(4 * f + r));
         else asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(hi) : "v"(bit), "i"(4 * f + r));
-#else
-        if (i == 0) lo |= bit << (4 * f + r);
-        else hi |= bit << (4 * f + r);
-#endif
     }
     __device__ __forceinline__ void store(u64* base) const {
         base[threadIdx.x & 63] = ((u64)hi << 32) | lo;
@@ -536,7 +549,9 @@ struct MaskRd {
 // polynomial x + x^3 P(x^2) (least-squares fit in relative error, <= 0.9 ulp in f32);
 // otherwise 1 - 2 / (1 + e^{2|x|}) (<= 2 ulp).  The fp32 mode keeps tanhf / sqrtf / IEEE
 // division (torch's arithmetic).  Parity: tests/test_gpu_*.py tolerances.
+// (every rounding step written out: no contraction left to the compiler)
 __device__ __forceinline__ float fast_tanh(float x) {
+#pragma clang fp contract(off)
     const float a = __builtin_fabsf(x);
     const float x2 = x * x;
     float p = -0.005691935773938894f;
@@ -546,10 +561,9 @@ __device__ __forceinline__ float fast_tanh(float x) {
     p = __builtin_fmaf(p, x2, -0.3333328068256378f);
     const float small = __builtin_fmaf(x * x2, p, x);
     const float e = __builtin_amdgcn_exp2f(a * 2.8853900817779268f);   // 2 log2(e)
-    const float big = __builtin_copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e), x);
+    const float big = __builtin_copysignf(__builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + e), 1.f), x);
     return a < 0.625f ? small : big;
 }
-
 // One element of the Adam tail (attack_utils.py:78-86, torch _single_tensor_adam): tanh'
 // of the reparameterisation, Adam moments and step, next adv = vc + eps*tanh(ptb).  One
 // definition for every engine, with the contraction pinned, so the fused and long engines

@@ -9,7 +9,7 @@ TAG="${TAG:-emb}"
 timeout -k 10 300 attack-vc_amd/avc_bench $WL > gpurun_out/kt_${TAG}_plain.log 2>&1
 rc=$?; echo "plain rc=$rc"; grep -E "ms_per_iter|ktime" gpurun_out/kt_${TAG}_plain.log; [ $rc -eq 0 ] || exit $rc
 rm -rf gpurun_out/kt_${TAG}_trace
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_${TAG}_trace -o run --output-format csv -- \
+AVC_BENCH_KTIME=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_${TAG}_trace -o run --output-format csv -- \
   attack-vc_amd/avc_bench $WL > gpurun_out/kt_${TAG}_traced.log 2>&1
 rc=$?; echo "traced rc=$rc"; grep -E "ms_per_iter|ktime" gpurun_out/kt_${TAG}_traced.log; [ $rc -eq 0 ] || exit $rc
 find gpurun_out/kt_${TAG}_trace -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/kt_${TAG}_kernel_stats.csv
