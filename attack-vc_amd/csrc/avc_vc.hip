@@ -36,6 +36,12 @@ AVC_KTIME_DEFINE(vc)     // dec_fwd_fused, dec_bwd_fused per precision (avc_ktim
 #ifndef AVC_DZ_RD_BWD
 #define AVC_DZ_RD_BWD 8
 #endif
+// dec_bwd_fused's d loss / d out staging: 16-byte loads with the channel fastest over the lanes, so
+// a wave's 2-byte LDS stores go to one image row (phase stamps of the kernel's start: 12.8k cycles
+// with the scalar loop, 18.7k with 16-byte loads frame-fastest -- 16-way conflicted stores -- 9.8k)
+#ifndef AVC_DZ_GIN_CO
+#define AVC_DZ_GIN_CO 1
+#endif
 
 namespace avc {
 
@@ -150,18 +156,11 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
     const int act = STD ? 0 : A.act;                   // the standard shape is ReLU (host-checked)
     const float* cond = A.cond + (size_t)b * (2 * nblk) * 256;
     const bool stash = A.stash_per_utt > 0;
+    FZ_PH_DECL
+    FZ_PH();
 
     char* HB = fz_lds;                       // block input image [Tn + 2P] rows
     char* YB = HB + (Tn + 2 * P) * RS;       // conv1 output image (first: the mu operand)
-
-    {   // mu [128][T0] -> YB rows t (operand of the 1x1 in_conv)
-        const float* mu = A.mu + (size_t)b * FZ_C * T0;
-        for (int idx = tid; idx < FZ_C * T0; idx += 256) {
-            const int ci = idx / T0, t = idx - ci * T0;
-            st1<PREC>(YB + t * RS + ci * ESZ, mu[idx]);
-        }
-    }
-    __syncthreads();
 
     const int ns_c = ks * FZ_C / KS;
     const int ns_1 = FZ_C / KS;
@@ -171,9 +170,52 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
     // out_conv: 80 rows = 5 tiles; waves take tiles {0,1}, {2,3}, {3,4}, {3,4} (the
     // duplicates are computed and dropped)
     auto op_out = [&]() __attribute__((always_inline)) { return aop(A.w.out, w < 2 ? 2 * w : 3, 2, ns_1, ns_1); };
+    // the in_conv weights first: their L2 round trip runs under the mu staging
     ARing<2, SH == 0 ? AVC_DZ_RD_FWD : 4> ring;
     ring_fill(ring, op_in());
     int rb[NF];
+
+    {   // mu [128][T0] -> YB rows t (operand of the 1x1 in_conv)
+        const float* mu = A.mu + (size_t)b * FZ_C * T0;
+        if constexpr (STD) {   // all loads in flight at once: 4 frames of one channel per 16 bytes
+            constexpr int NV = FZ_C * StdDec::T0 / 4 / 256;
+            f32x4 m[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) m[k] = reinterpret_cast<const f32x4*>(mu)[tid + 256 * k];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                const int idx = 4 * (tid + 256 * k), ci = idx / StdDec::T0, t = idx - ci * StdDec::T0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) st1<PREC>(YB + (t + e) * RS + ci * ESZ, m[k][e]);
+            }
+        } else {
+            for (int idx = tid; idx < FZ_C * T0; idx += 256) {
+                const int ci = idx / T0, t = idx - ci * T0;
+                st1<PREC>(YB + t * RS + ci * ESZ, mu[idx]);
+            }
+        }
+    }
+    __syncthreads();
+
+    // e2e: the targets of the output loss, all in flight at once.  (Loaded after the last block's
+    // conv2 GEMM or after its epilogue instead, A/B on the e2e iteration: the kernel 0.9-1.2 us
+    // shorter, the iteration 0.4-0.9 % longer -- loaded here.)
+    const bool e2e = A.tgt_out != nullptr;
+    const size_t obase4 = (size_t)b * DZ_COUT * Tn / 4;     // 80*Tn is a multiple of 4
+    const int n4 = DZ_COUT * Tn / 4;
+    constexpr int OV = (DZ_COUT * 128 / 4 + 255) / 256;     // f32x4 per thread at Tn <= 128
+    f32x4 tv[OV], ov[OV];
+    auto tgt_load = [&]() __attribute__((always_inline)) {
+        if (!e2e) return;
+        const f32x4* tg4 = reinterpret_cast<const f32x4*>(A.tgt_out) + obase4;
+        const f32x4* og4 = reinterpret_cast<const f32x4*>(A.org_out) + obase4;
+#pragma unroll
+        for (int k = 0; k < OV; ++k) {
+            const int q = min(tid + 256 * k, n4 - 1);
+            tv[k] = tg4[q];
+            ov[k] = og4[q];
+        }
+    };
 
     // AdaIN (append_cond) of IN layer q on the normalised rows: z = yhat * std + mean.  The
     // conditions (and the layer's bias) are loaded ahead of the GEMM that precedes their use,
@@ -225,6 +267,7 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
             fz_gemm<PREC, 2, NF, FZ_C, 1>(hres, IC<StdDec::nf(StdDec::T0)>{}, ring, op_in(), op_c1(0), YB, rb);
         else
             fz_gemm<PREC, 2, NF, FZ_C, 1>(hres, IC<NF>{}, ring, op_in(), op_c1(0), YB, rb);
+        FZ_PH();
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const f32x4 bi = *reinterpret_cast<const f32x4*>(A.w.b_in + ch0 + 16 * i);
@@ -258,6 +301,7 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
         Cnd k1;
         if constexpr (STD) k1 = cnd_load(2 * l, A.w.b_c1[l], nullptr);
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c1(l), op_c2(l, 0), HB, rb);
+        FZ_PH();
         if constexpr (!STD) k1 = cnd_load(2 * l, A.w.b_c1[l], nullptr);
         {
 #pragma unroll
@@ -277,7 +321,9 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
                     if (f < nfi && t < Ti) put_reflect<PREC>(YB, t, Ti, P, (ch0 + 16 * i) * ESZ, acc[i][f]);
                 }
         }
+        FZ_PH();
         __syncthreads();
+        FZ_PH();
         const AOp nxt = l + 1 < nblk ? op_c1(l + 1) : op_out();
         Cnd k2;
         auto k2_load = [&]() __attribute__((always_inline)) {
@@ -287,6 +333,7 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
         if (up == 1) {
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c2(l, 0), nxt, YB, rb);
+            FZ_PH();
             if constexpr (!STD) k2_load();
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -312,6 +359,7 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
             zero_acc(a1);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfi, ring, op_c2(l, 0), op_c2(l, 1), YB, rb);
             fz_gemm<PREC, 2, NF, FZ_C, 1>(a1, nfi, ring, op_c2(l, 1), nxt, YB, rb);
+            FZ_PH();
             if constexpr (!STD) k2_load();
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -356,7 +404,9 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
                     }
             }
         }
+        FZ_PH();
         __syncthreads();
+        FZ_PH();
     };
     if constexpr (STD != 0) {
         static_for<0, StdDec::NBLK>([&](auto L) __attribute__((always_inline)) {
@@ -376,6 +426,7 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<StdDec::nf(StdDec::Tl(StdDec::NBLK))>{}, ring, op_out(), op_out(), HB, rb);
     else
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, IC<NF>{}, ring, op_out(), op_out(), HB, rb);
+    FZ_PH();
     // o = out_conv + b -> LDS [80][Tn] fp32 (HB / YB are free once every wave is past
     // the GEMM), then all 256 threads finish with 16-byte, batched global accesses
     __syncthreads();
@@ -398,33 +449,22 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
         }
     }
     __syncthreads();
-    const bool e2e = A.tgt_out != nullptr;
-    const size_t obase4 = (size_t)b * DZ_COUT * Tn / 4;     // 80*Tn is a multiple of 4
-    const int n4 = DZ_COUT * Tn / 4;
     const f32x4* OS4 = reinterpret_cast<const f32x4*>(OS);
-    f32x4* out4 = reinterpret_cast<f32x4*>(A.out) + obase4;
+    // (e2e iterations pass no output buffer: only the loss gradient leaves the kernel)
+    f32x4* out4 = A.out ? reinterpret_cast<f32x4*>(A.out) + obase4 : nullptr;
     const float gscale = e2e ? A.scal[2] : 0.f;
     float q1 = 0.f, q2 = 0.f;
-    constexpr int OV = (DZ_COUT * 128 / 4 + 255) / 256;     // f32x4 per thread at Tn <= 128
     if (!e2e) {
         for (int q = tid; q < n4; q += 256) out4[q] = OS4[q];
     } else {
-        const f32x4* tg4 = reinterpret_cast<const f32x4*>(A.tgt_out) + obase4;
-        const f32x4* og4 = reinterpret_cast<const f32x4*>(A.org_out) + obase4;
         f32x4* g4 = reinterpret_cast<f32x4*>(A.g_out) + obase4;
-        f32x4 tv[OV], ov[OV];
-#pragma unroll
-        for (int k = 0; k < OV; ++k) {
-            const int q = min(tid + 256 * k, n4 - 1);
-            tv[k] = tg4[q];
-            ov[k] = og4[q];
-        }
+        tgt_load();
 #pragma unroll
         for (int k = 0; k < OV; ++k) {
             const int q = tid + 256 * k;
             if (q >= n4) continue;
             const f32x4 o = OS4[q];
-            out4[q] = o;
+            if (out4) out4[q] = o;
             // MSE(out, tgt) - 0.1 MSE(out, org) (attack_utils.py:41-43) and its gradient
             f32x4 g;
 #pragma unroll
@@ -458,6 +498,8 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
             A.losses[(size_t)(step - 1) * A.B + b] = s1 / n - 0.1f * (s2 / n);
         }
     }
+    FZ_PH();
+    FZ_PH_DUMP("dfwd");
 }
 template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) dec_fwd_fused(DecArgs A) {
@@ -495,27 +537,62 @@ __device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
     char* GB2 = GB + (Tn + 2 * ZP) * RS;        // dY image of half 1 / the out_conv^T operand
     float* FSCR = reinterpret_cast<float*>(GB2 + (Tn + 2 * ZP) * RS) + w * DZ_FOLD_FLOATS;
     const int n16 = (Tn + 2 * ZP) * RS / 16;
-
-    // both images zero: pad rows, stale frames and the K padding of out_conv^T (80 -> KS)
-    for (int i = tid; i < 2 * n16; i += 256) reinterpret_cast<f32x4*>(GB)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    __syncthreads();
-    {   // g_in [80][Tn] -> GB2 rows t
-        const float* g = A.g_in + (size_t)b * DZ_COUT * Tn;
-        for (int idx = tid; idx < DZ_COUT * Tn; idx += 256) {
-            const int co = idx / Tn, t = idx - co * Tn;
-            st1<PREC>(GB2 + t * RS + co * ESZ, g[idx]);
-        }
-    }
-    __syncthreads();
+    FZ_PH_DECL
+    FZ_PH();
 
     const int ns_c = ks * FZ_C / KS;
     const int ns_o = (DZ_COUT + KS - 1) / KS;
     auto op_outT = [&]() __attribute__((always_inline)) { return aop(A.w.outT, 2 * w, 2, ns_o, ns_o); };
     auto op_c1T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c1T[l], 2 * w, 2, ns_c, ns_c); };
     auto op_c2T = [&](int l, int s) __attribute__((always_inline)) { return aop(A.w.c2T[l][s], 2 * w, 2, ns_c, ns_c); };
+    // the out_conv^T weights first, then d loss / d out: both round trips run under the LDS clear
     ARing<2, SH == 0 ? AVC_DZ_RD_BWD : 4> ring;
     ring_fill(ring, op_outT());
     int rb[NF];
+
+    const float* gin = A.g_in + (size_t)b * DZ_COUT * Tn;
+    constexpr int GV = STD ? DZ_COUT * StdDec::Tl(StdDec::NBLK) / 4 / 256 : 1;   // 16-byte loads per thread
+    f32x4 gv[GV];
+    constexpr int TN = StdDec::Tl(StdDec::NBLK);
+    // 16-byte chunk q of this thread: (channel, 4-frame group); AVC_DZ_GIN_CO: channels fastest over
+    // the lanes, so a wave's 2-byte LDS stores land in one row
+    auto gin_q = [&](int k, int& co, int& t) __attribute__((always_inline)) {
+        const int q = tid + 256 * k;
+        if (AVC_DZ_GIN_CO) {
+            co = q % DZ_COUT;
+            t = 4 * (q / DZ_COUT);
+        } else {
+            co = q / (TN / 4);
+            t = 4 * (q - co * (TN / 4));
+        }
+    };
+    if constexpr (STD) {
+#pragma unroll
+        for (int k = 0; k < GV; ++k) {
+            int co, t;
+            gin_q(k, co, t);
+            gv[k] = *reinterpret_cast<const f32x4*>(gin + co * TN + t);
+        }
+    }
+    // both images zero: pad rows, stale frames and the K padding of out_conv^T (80 -> KS)
+    for (int i = tid; i < 2 * n16; i += 256) reinterpret_cast<f32x4*>(GB)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    // g_in [80][Tn] -> GB2 rows t
+    if constexpr (STD) {
+#pragma unroll
+        for (int k = 0; k < GV; ++k) {
+            int co, t;
+            gin_q(k, co, t);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) st1<PREC>(GB2 + (t + e) * RS + co * ESZ, gv[k][e]);
+        }
+    } else {
+        for (int idx = tid; idx < DZ_COUT * Tn; idx += 256) {
+            const int co = idx / Tn, t = idx - co * Tn;
+            st1<PREC>(GB2 + t * RS + co * ESZ, gin[idx]);
+        }
+    }
+    __syncthreads();
 
     // what the AdaIN / IN backward of IN layer q reads from memory -- the conditions, 1/std and
     // the stashed normalised activations (H halves x nfq fragments) -- loaded one GEMM ahead of
@@ -565,9 +642,11 @@ __device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
     else
         fz_gemm<PREC, 2, NF, DZ_COUT, 1>(gh, IC<8>{}, ring, op_outT(), op_c2T(nblk - 1, 0), GB2, rb);
     __syncthreads();
+    FZ_PH();
     // GB2 becomes the half-1 dY image: clear the out_conv^T operand
     for (int i = tid; i < n16; i += 256) reinterpret_cast<f32x4*>(GB2)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
+    FZ_PH();
 
     // act + AdaIN + InstanceNorm backward of IN layer q over H halves of T frames, in
     // place on g0 (half 0) / g1 (half 1):  z = yhat*std + mean,  g_z = g * act'(z),
@@ -687,7 +766,9 @@ __device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
             }
         zero_rows<PREC>(GB, ZP + Ti, ZP, w);      // frames past Ti (stale from longer layers)
         if (up == 2) zero_rows<PREC>(GB2, ZP + Ti, ZP, w);
+        FZ_PH();
         __syncthreads();
+        FZ_PH();
         // conv2^T (both halves) over Ti interior frames + 2P pad positions, then the
         // reflect-pad adjoint
         const int ncol = Ti + 2 * P;
@@ -706,7 +787,9 @@ __device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
         } else {
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c2T(l, 0), after, GB, rb);
         }
+        FZ_PH();
         fold_edges(acc, Ti, P, FSCR);   // (barrier: GB / GB2 are free afterwards)
+        FZ_PH();
         if constexpr (!STD) pf = adn_load(2 * l, 1, Ti);
         // conv1 branch: act, AdaIN(2l), IN backward; then conv1^T into the residual
         // (the first block's conv1 input is the in_conv output: mu is constant, stop)
@@ -719,12 +802,16 @@ __device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
                     const int t = 16 * f + c;
                     if (f < nfq && t < Ti) st4<PREC>(GB + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, acc[i][f]);
                 }
+            FZ_PH();
             __syncthreads();
+            FZ_PH();
             // the next block's conv2 branch, under this conv1^T GEMM
             if constexpr (STD) pf = adn_load(2 * (l - 1) + 1, StdDec::up(l - 1), StdDec::Tl(l - 1));
             zero_acc(acc);
             fz_gemm<PREC, 2, NF, FZ_C, -1>(acc, nfc, ring, op_c1T(l), op_c2T(l - 1, 0), GB, rb);
+            FZ_PH();
             fold_edges(acc, Ti, P, FSCR);
+            FZ_PH();
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -743,6 +830,8 @@ __device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
     } else {
         for (int l = nblk - 1; l >= 0; --l) block(IC<FZ_MAXNF>{}, l, A.Tl[l], A.up[l]);
     }
+    FZ_PH();
+    FZ_PH_DUMP("dbwd");
 }
 template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) dec_bwd_fused(DecArgs A) {
