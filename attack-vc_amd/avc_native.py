@@ -14,7 +14,8 @@ from typing import Dict, Optional, Tuple
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libavc.so")
+# (AVC_LIB_PATH: another libavc build, for A/B timing of kernel variants)
+LIB_PATH = os.environ.get("AVC_LIB_PATH") or os.path.join(_HERE, "libavc.so")
 MAX_BLOCKS = 16
 
 PREC = {"fp32": 0, "bf16": 1}

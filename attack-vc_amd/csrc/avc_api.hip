@@ -59,7 +59,9 @@ template <int CO>
 __global__ void pm_cin1(PmConvArgs P);
 template <int CI>
 __global__ void pm_cout1(PmConvArgs P);
-template <int MT>
+template <int CI>
+__global__ void pm_cout1h(PmConvArgs P);
+template <int MT, int MODE>
 __global__ void pm_mfma(PmConvArgs P);
 __global__ void vsm_gather(VsmArgs A);
 __global__ void vsm_combine(VsmArgs A);

@@ -290,6 +290,90 @@ __global__ void __launch_bounds__(256) pm_cout1(PmConvArgs P) {
         P.y[((size_t)b * P.Ho + oy) * P.Wo + ox] = pm_act(v + P.bias[0], P);
     }
 }
+// pm_cout1 when its two K slices split every class at ci = CI / 2 (CI = 32, ksplit 2: the
+// reference network at any batch): the input channels in two halves, slice h = channels of half h,
+// so a workgroup stages and holds half the pixel vectors at a time -- 33 KB of LDS and ~100
+// registers instead of 57 KB and 260 (four workgroups per CU instead of one, so one workgroup's
+// staging round trip runs under another's FMA chains).  Per output the same fmaf chains and the
+// same slice sum (0 + slice 0) + slice 1 as pm_cout1: bitwise the same results.
+template <int CI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) pm_cout1h(PmConvArgs P) {
+    constexpr int CH = CI / 2, XS = CH + 4, XCAP = 384;
+    __shared__ float Ws[4][4 * CI];
+    __shared__ __attribute__((aligned(16))) float xs[XCAP * XS];
+    for (int c = 0; c < 4; ++c) {
+        const int K = CI * ((c >> 1) == 0 ? 2 : 1) * ((c & 1) == 0 ? 2 : 1);
+        for (int i = threadIdx.x; i < K; i += 256) Ws[c][i] = P.w[P.woff[c] + i];
+    }
+    const int Hq = (P.Ho + 1) / 2, Wq = (P.Wo + 1) / 2;
+    const int N = P.B * Hq * Wq, HWq = Hq * Wq, HWin = P.Hin * P.Win;
+    const int n0 = blockIdx.x * 256, n1 = min(N - 1, n0 + 255);
+    const int bf = n0 / HWq, qyf = (n0 - bf * HWq) / Wq, bl = n1 / HWq, qyl = (n1 - bl * HWq) / Wq;
+    const long p_lo = (long)bf * HWin + (long)max(qyf - 1, 0) * P.Win;
+    const long p_hi = (long)bl * HWin + (long)min(qyl, P.Hin - 1) * P.Win + P.Win - 1;
+    const int cnt = (int)(p_hi - p_lo + 1);
+    const bool staged = cnt <= XCAP;                    // workgroup-uniform
+    const int n = n0 + threadIdx.x;
+    const bool live = n < N;
+    const int nn = live ? n : N - 1;
+    const int b = nn / HWq;
+    const int r = nn - b * HWq;
+    const int qy = r / Wq, qx = r - qy * Wq;
+    const float* __restrict__ xb = P.x + (size_t)b * CI * HWin;
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+        if (h) __syncthreads();                         // every lane is done with half 0
+        if (staged) {
+            const f32x4* src = reinterpret_cast<const f32x4*>(P.x + p_lo * CI + h * CH);
+            for (int i = threadIdx.x; i < cnt * (CH / 4); i += 256) {
+                const int pix = i / (CH / 4), q = i - pix * (CH / 4);
+                *reinterpret_cast<f32x4*>(xs + pix * XS + 4 * q) = src[pix * (CI / 4) + q];
+            }
+        }
+        __syncthreads();
+        f32x4 xv[2][2][CH / 4];
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+                const int iy = qy - dy, ix = qx - dx;
+                const bool ok = iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
+                const int pi = ok ? iy * P.Win + ix : 0;
+                const int li = ok ? (int)((long)b * HWin + pi - p_lo) : 0;
+                const f32x4* src = staged ? reinterpret_cast<const f32x4*>(xs + li * XS)
+                                          : reinterpret_cast<const f32x4*>(xb + (size_t)pi * CI + h * CH);
+#pragma unroll
+                for (int q = 0; q < CH / 4; ++q) xv[dy][dx][q] = ok ? src[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+        for (int cls = 0; cls < 4; ++cls) {
+            const int py = cls >> 1, px = cls & 1;
+            const int nty = py == 0 ? 2 : 1, ntx = px == 0 ? 2 : 1, nt = nty * ntx;
+            float acc = 0.f;
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                const int ci = h * CH + c;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (t >= nt) continue;
+                    const int ta = ntx == 2 ? t >> 1 : t, tc = ntx == 2 ? t & 1 : 0;
+                    const int dy = py == 0 ? ta : 0, dx = px == 0 ? tc : 0;
+                    acc = fmaf(Ws[cls][ci * nt + t], xv[dy][dx][c >> 2][c & 3], acc);
+                }
+            }
+            part[cls] += acc;                           // (0 + slice 0) + slice 1, as pm_cout1
+        }
+    }
+    if (!live) return;
+#pragma unroll
+    for (int cls = 0; cls < 4; ++cls) {
+        const int oy = 2 * qy + (cls >> 1), ox = 2 * qx + (cls & 1);
+        if (oy >= P.Ho || ox >= P.Wo) continue;
+        P.y[((size_t)b * P.Ho + oy) * P.Wo + ox] = pm_act(part[cls] + P.bias[0], P);
+    }
+}
+template __global__ void pm_cout1h<32>(PmConvArgs);
 template __global__ void pm_cin1<32>(PmConvArgs);
 template __global__ void pm_cout1<32>(PmConvArgs);
 
@@ -317,17 +401,32 @@ __global__ void __launch_bounds__(256) pm_reduce(PmConvArgs P) {
 // next chunk's fragments are in flight during the current chunk's MFMAs.  Per output the
 // summation order is fixed by the layer's (geometry-only) K split: batch-invariant.
 // ---------------------------------------------------------------------------------
-template <int MT>
-__global__ void __launch_bounds__(256) pm_mfma(PmConvArgs P) {
+// The K loop keeps the next chunk's fragments in flight under the current chunk's MFMAs only if
+// the waitcnt pass can count them: no branch inside the loop (the mode is a template parameter,
+// every load is unconditional -- invalid taps read a clamped in-range address and are zeroed after
+// the load, the last prefetch re-reads the final chunk).  With the mode a runtime value and
+// conditional loads, every wait in the loop was vmcnt(0): the prefetch waited for itself.
+// occupancy cap (amdgpu_waves_per_eu): off -- forcing 4 waves per SIMD (<= 128 VGPRs; the MT = 4 forms
+// take 116-130 unconstrained) measured 291.7k vs 295.8k windows/s unconstrained
+#ifndef AVC_PM_WPE
+#define AVC_PM_WPE 0
+#endif
+#if AVC_PM_WPE
+#define PM_MFMA_ATTR __attribute__((amdgpu_waves_per_eu(AVC_PM_WPE)))
+#else
+#define PM_MFMA_ATTR
+#endif
+template <int MT, int MODE>
+__global__ void __launch_bounds__(256) PM_MFMA_ATTR pm_mfma(PmConvArgs P) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 15, q = lane >> 4;
     const int ks = P.ksplit > 1 ? P.ksplit : 1;
     const int cls = blockIdx.z / ks, slice = blockIdx.z - cls * ks;
     const int py = cls >> 1, px = cls & 1;
-    const int nty = P.mode == 1 ? (py == 0 ? 2 : 1) : 3;
-    const int ntx = P.mode == 1 ? (px == 0 ? 2 : 1) : 3;
-    const int Hq = P.mode == 1 ? (P.Ho - py + 1) / 2 : P.Ho;
-    const int Wq = P.mode == 1 ? (P.Wo - px + 1) / 2 : P.Wo;
+    const int nty = MODE == 1 ? (py == 0 ? 2 : 1) : 3;
+    const int ntx = MODE == 1 ? (px == 0 ? 2 : 1) : 3;
+    const int Hq = MODE == 1 ? (P.Ho - py + 1) / 2 : P.Ho;
+    const int Wq = MODE == 1 ? (P.Wo - px + 1) / 2 : P.Wo;
     const int N = P.B * Hq * Wq;
     const int nbase = blockIdx.x * 128;
     if (nbase >= N) return;                     // (uniform: class grids are padded to the largest)
@@ -337,7 +436,7 @@ __global__ void __launch_bounds__(256) pm_mfma(PmConvArgs P) {
     const int kc0 = slice * cps, kc1 = min(nchunk, kc0 + cps);
     const int mt0 = blockIdx.y * MT;            // first M tile of this workgroup
     const int nmt = (P.Cout + 15) >> 4;
-    // this lane's two output columns
+    // this lane's two output columns (an invalid column computes on column 0 and is not stored)
     int cb[2], cy[2], cx[2];
     bool cv[2];
 #pragma unroll
@@ -364,8 +463,8 @@ __global__ void __launch_bounds__(256) pm_mfma(PmConvArgs P) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             int iy, ix;
-            bool ok = cv[j];
-            if (P.mode == 0) {
+            bool ok = true;
+            if constexpr (MODE == 0) {
                 iy = cy[j] * P.sh + a - 1;
                 ix = cx[j] * P.sw + bb - 1;
                 iy = iy < 0 ? -iy : (iy >= P.Hin ? 2 * (P.Hin - 1) - iy : iy);
@@ -373,10 +472,12 @@ __global__ void __launch_bounds__(256) pm_mfma(PmConvArgs P) {
             } else {
                 iy = py == 0 ? cy[j] - a : cy[j];
                 ix = px == 0 ? cx[j] - bb : cx[j];
-                ok = ok && iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
+                ok = iy >= 0 && iy < P.Hin && ix >= 0 && ix < P.Win;
+                iy = min(max(iy, 0), P.Hin - 1);
+                ix = min(max(ix, 0), P.Win - 1);
             }
-            b[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (ok) b[j] = *reinterpret_cast<const f32x4*>(P.x + (((size_t)cb[j] * P.Hin + iy) * P.Win + ix) * P.Cin + ci);
+            const f32x4 v = *reinterpret_cast<const f32x4*>(P.x + (((size_t)cb[j] * P.Hin + iy) * P.Win + ix) * P.Cin + ci);
+            b[j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
     f32x4 acc[MT][2];
@@ -384,7 +485,6 @@ __global__ void __launch_bounds__(256) pm_mfma(PmConvArgs P) {
     for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 a0[MT], a1[MT], b0[2], b1[2];
     auto mma = [&](const f32x4 (&a)[MT], const f32x4 (&b)[2]) __attribute__((always_inline)) {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
@@ -393,29 +493,29 @@ __global__ void __launch_bounds__(256) pm_mfma(PmConvArgs P) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
     };
-    if (kc0 < kc1) {
+    if (kc0 < kc1) {   // (uniform; an empty K slice stores its zeros like any other)
+        f32x4 a0[MT], a1[MT], b0[2], b1[2];
         load_a(kc0, a0);
         load_b(kc0, b0);
-    }
-    int kc = kc0;
-    for (; kc + 1 < kc1; kc += 2) {
-        load_a(kc + 1, a1);
-        load_b(kc + 1, b1);
-        mma(a0, b0);
-        if (kc + 2 < kc1) {
-            load_a(kc + 2, a0);
-            load_b(kc + 2, b0);
+        int kc = kc0;
+        for (; kc + 1 < kc1; kc += 2) {
+            load_a(kc + 1, a1);
+            load_b(kc + 1, b1);
+            mma(a0, b0);
+            const int kn = min(kc + 2, kc1 - 1);    // (the last round re-reads the final chunk)
+            load_a(kn, a0);
+            load_b(kn, b0);
+            mma(a1, b1);
         }
-        mma(a1, b1);
+        if (kc < kc1) mma(a0, b0);
     }
-    if (kc < kc1) mma(a0, b0);
     // epilogue: rows 4q + r of M tile i = 4 consecutive output channels of column (j, c): NHWC
     const size_t per = (size_t)P.B * P.Cout * P.Ho * P.Wo;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         if (!cv[j]) continue;
-        const int oy = P.mode == 1 ? 2 * cy[j] + py : cy[j];
-        const int ox = P.mode == 1 ? 2 * cx[j] + px : cx[j];
+        const int oy = MODE == 1 ? 2 * cy[j] + py : cy[j];
+        const int ox = MODE == 1 ? 2 * cx[j] + px : cx[j];
         const size_t pix = ((size_t)cb[j] * P.Ho + oy) * P.Wo + ox;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
@@ -433,8 +533,10 @@ __global__ void __launch_bounds__(256) pm_mfma(PmConvArgs P) {
         }
     }
 }
-template __global__ void pm_mfma<2>(PmConvArgs);
-template __global__ void pm_mfma<4>(PmConvArgs);
+template __global__ void pm_mfma<2, 0>(PmConvArgs);
+template __global__ void pm_mfma<2, 1>(PmConvArgs);
+template __global__ void pm_mfma<4, 0>(PmConvArgs);
+template __global__ void pm_mfma<4, 1>(PmConvArgs);
 
 // ---- VSMask protect loop (/root/reference/vsmask.py:177-208) ----------------------------
 // The reference walks start = 0, S, 2S, ... < T - W, feeds mel[..., start:start+W] (always the
