@@ -61,7 +61,7 @@ template <int CI>
 __global__ void pm_cout1(PmConvArgs P);
 template <int CI>
 __global__ void pm_cout1h(PmConvArgs P);
-template <int MT, int MODE>
+template <int MT, int MODE, int NT>
 __global__ void pm_mfma(PmConvArgs P);
 __global__ void vsm_gather(VsmArgs A);
 __global__ void vsm_combine(VsmArgs A);

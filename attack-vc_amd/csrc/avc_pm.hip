@@ -406,6 +406,9 @@ __global__ void __launch_bounds__(256) pm_reduce(PmConvArgs P) {
 // every load is unconditional -- invalid taps read a clamped in-range address and are zeroed after
 // the load, the last prefetch re-reads the final chunk).  With the mode a runtime value and
 // conditional loads, every wait in the loop was vmcnt(0): the prefetch waited for itself.
+#ifndef AVC_PM_PF
+#define AVC_PM_PF 1
+#endif
 // occupancy cap (amdgpu_waves_per_eu): off -- forcing 4 waves per SIMD (<= 128 VGPRs; the MT = 4 forms
 // take 116-130 unconstrained) measured 291.7k vs 295.8k windows/s unconstrained
 #ifndef AVC_PM_WPE
@@ -416,7 +419,7 @@ __global__ void __launch_bounds__(256) pm_reduce(PmConvArgs P) {
 #else
 #define PM_MFMA_ATTR
 #endif
-template <int MT, int MODE>
+template <int MT, int MODE, int NT>
 __global__ void __launch_bounds__(256) PM_MFMA_ATTR pm_mfma(PmConvArgs P) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 15, q = lane >> 4;
@@ -428,7 +431,7 @@ __global__ void __launch_bounds__(256) PM_MFMA_ATTR pm_mfma(PmConvArgs P) {
     const int Hq = MODE == 1 ? (P.Ho - py + 1) / 2 : P.Ho;
     const int Wq = MODE == 1 ? (P.Wo - px + 1) / 2 : P.Wo;
     const int N = P.B * Hq * Wq;
-    const int nbase = blockIdx.x * 128;
+    const int nbase = blockIdx.x * 64 * NT;
     if (nbase >= N) return;                     // (uniform: class grids are padded to the largest)
     const int ccpt = P.Cin >> 4;                // K chunks per tap
     const int nchunk = nty * ntx * ccpt;
@@ -437,11 +440,11 @@ __global__ void __launch_bounds__(256) PM_MFMA_ATTR pm_mfma(PmConvArgs P) {
     const int mt0 = blockIdx.y * MT;            // first M tile of this workgroup
     const int nmt = (P.Cout + 15) >> 4;
     // this lane's two output columns (an invalid column computes on column 0 and is not stored)
-    int cb[2], cy[2], cx[2];
-    bool cv[2];
+    int cb[NT], cy[NT], cx[NT];
+    bool cv[NT];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = nbase + 32 * w + 16 * j + c;
+    for (int j = 0; j < NT; ++j) {
+        const int n = nbase + 16 * NT * w + 16 * j + c;
         cv[j] = n < N;
         const int nn = cv[j] ? n : 0;
         cb[j] = nn / (Hq * Wq);
@@ -457,11 +460,11 @@ __global__ void __launch_bounds__(256) PM_MFMA_ATTR pm_mfma(PmConvArgs P) {
             a[i] = Aw[((size_t)mt * nchunk + kc) * 64 + lane];
         }
     };
-    auto load_b = [&](int kc, f32x4 (&b)[2]) __attribute__((always_inline)) {
+    auto load_b = [&](int kc, f32x4 (&b)[NT]) __attribute__((always_inline)) {
         const int tap = kc / ccpt, ci = ((kc - tap * ccpt) << 4) + 4 * q;
         const int a = tap / ntx, bb = tap - a * ntx;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NT; ++j) {
             int iy, ix;
             bool ok = true;
             if constexpr (MODE == 0) {
@@ -480,39 +483,52 @@ __global__ void __launch_bounds__(256) PM_MFMA_ATTR pm_mfma(PmConvArgs P) {
             b[j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
-    f32x4 acc[MT][2];
+    f32x4 acc[MT][NT];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mma = [&](const f32x4 (&a)[MT], const f32x4 (&b)[2]) __attribute__((always_inline)) {
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mma = [&](const f32x4 (&a)[MT], const f32x4 (&b)[NT]) __attribute__((always_inline)) {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
     };
+    // the epilogue's biases, loaded now so their round trip is hidden by the K loop
+    f32x4 bias4[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+        bias4[i] = *reinterpret_cast<const f32x4*>(P.bias + min((mt0 + i) * 16 + 4 * q, P.Cout - 4));
     if (kc0 < kc1) {   // (uniform; an empty K slice stores its zeros like any other)
-        f32x4 a0[MT], a1[MT], b0[2], b1[2];
-        load_a(kc0, a0);
-        load_b(kc0, b0);
-        int kc = kc0;
-        for (; kc + 1 < kc1; kc += 2) {
-            load_a(kc + 1, a1);
-            load_b(kc + 1, b1);
-            mma(a0, b0);
-            const int kn = min(kc + 2, kc1 - 1);    // (the last round re-reads the final chunk)
-            load_a(kn, a0);
-            load_b(kn, b0);
-            mma(a1, b1);
+        // ring of PF + 1 chunk buffers, PF chunks in flight ahead of the one being multiplied;
+        // prefetch indices clamped to the slice (the last rounds re-read its final chunk)
+        constexpr int PF = AVC_PM_PF, NB = PF + 1;
+        f32x4 ra[NB][MT], rb[NB][NT];
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            load_a(min(kc0 + p, kc1 - 1), ra[p]);
+            load_b(min(kc0 + p, kc1 - 1), rb[p]);
         }
-        if (kc < kc1) mma(a0, b0);
+        int kc = kc0;
+        for (; kc + NB <= kc1; kc += NB) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int kn = min(kc + u + PF, kc1 - 1);
+                load_a(kn, ra[(u + PF) % NB]);
+                load_b(kn, rb[(u + PF) % NB]);
+                mma(ra[u], rb[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PF; ++u)   // the last kc1 - kc <= PF chunks, already in flight
+            if (kc + u < kc1) mma(ra[u], rb[u]);
     }
     // epilogue: rows 4q + r of M tile i = 4 consecutive output channels of column (j, c): NHWC
     const size_t per = (size_t)P.B * P.Cout * P.Ho * P.Wo;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NT; ++j) {
         if (!cv[j]) continue;
         const int oy = MODE == 1 ? 2 * cy[j] + py : cy[j];
         const int ox = MODE == 1 ? 2 * cx[j] + px : cx[j];
@@ -527,16 +543,21 @@ __global__ void __launch_bounds__(256) PM_MFMA_ATTR pm_mfma(PmConvArgs P) {
             } else {
                 f32x4 v;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = pm_act(acc[i][j][r] + P.bias[co + r], P);
+                for (int r = 0; r < 4; ++r) v[r] = pm_act(acc[i][j][r] + bias4[i][r], P);
                 *reinterpret_cast<f32x4*>(P.y + o) = v;
             }
         }
     }
 }
-template __global__ void pm_mfma<2, 0>(PmConvArgs);
-template __global__ void pm_mfma<2, 1>(PmConvArgs);
-template __global__ void pm_mfma<4, 0>(PmConvArgs);
-template __global__ void pm_mfma<4, 1>(PmConvArgs);
+#define AVC_PM_INST(MT, NT)                                    \
+    template __global__ void pm_mfma<MT, 0, NT>(PmConvArgs);   \
+    template __global__ void pm_mfma<MT, 1, NT>(PmConvArgs);
+AVC_PM_INST(2, 1)
+AVC_PM_INST(2, 2)
+AVC_PM_INST(4, 1)
+AVC_PM_INST(4, 2)
+AVC_PM_INST(4, 4)
+#undef AVC_PM_INST
 
 // ---- VSMask protect loop (/root/reference/vsmask.py:177-208) ----------------------------
 // The reference walks start = 0, S, 2S, ... < T - W, feeds mel[..., start:start+W] (always the
