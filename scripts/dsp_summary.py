@@ -32,7 +32,7 @@ def main():
     dur = defaultdict(list)
     for r in csv.DictReader(open(one(f"{a.dir}/trace/**/run_kernel_trace.csv"))):
         if "dsp_" in r["Kernel_Name"]:
-            dur[r["Kernel_Name"].split("(")[0].replace("avc::", "")].append(
+            dur[r["Kernel_Name"].split("(")[0].replace("avc::", "").replace("void ", "").split("<")[0]].append(
                 (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     ctr = defaultdict(lambda: defaultdict(list))
     for i in (1, 2, 3):
@@ -41,7 +41,7 @@ def main():
         for r in csv.DictReader(open(one(f"{a.dir}/pmc_{i}/**/run_counter_collection.csv"))):
             d = r["Dispatch_Id"]
             per[d][r["Counter_Name"]] = per[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-            name[d] = r["Kernel_Name"].split("(")[0].replace("avc::", "")
+            name[d] = r["Kernel_Name"].split("(")[0].replace("avc::", "").replace("void ", "").split("<")[0]
         for d, cs in per.items():
             if "dsp_" in name[d]:
                 for c, v in cs.items():
