@@ -479,7 +479,7 @@ static int set_fused_attrs() {
     {(const void*)se_fwd_fused<PREC_F32, SH>, fz_lds_fwd(PREC_F32, 128, 5)},                \
         {(const void*)se_fwd_fused<PREC_BF16, SH>, fz_lds_fwd(PREC_BF16, 128, 5)},   \
         {(const void*)se_bwd_fused<PREC_F32, SH>, fz_lds_bwd(PREC_F32, 128)},                \
-        {(const void*)se_bwd_fused<PREC_BF16, SH>, fz_lds_bwd(PREC_BF16, 128)}
+        {(const void*)se_bwd_fused<PREC_BF16, SH>, fz_lds_bwd_launch(PREC_BF16, 128, SH, 25 * FZ_MASK_WORDS_PER_LAYER)}
     const std::pair<const void*, int> fns[] = {AVC_FZ_FNS(0), AVC_FZ_FNS(1), AVC_FZ_FNS(2), AVC_FZ_FNS(4),
                                                AVC_FZ_FNS(8)};
 #undef AVC_FZ_FNS
@@ -1261,10 +1261,10 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
     L.prec = prec;
     L.grid = dim3(ws.B);
     L.block = dim3(256);
-    L.shmem = ws.lz ? LZ_SHMEM : fz_lds_bwd(prec, ws.T);
     L.fz = fused_args(ctx, ws, prec);
     L.lz = ws.lza;
     L.fz_shape = fused_shape(ctx, ws.T);
+    L.shmem = ws.lz ? LZ_SHMEM : fz_lds_bwd_launch(prec, ws.T, L.fz_shape, L.fz.mask_words);
     AdamArgs& A = L.fz.adam;
     A.ptb = ws.ptb.p;
     A.m = ws.m.p;

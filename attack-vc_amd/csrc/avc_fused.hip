@@ -42,6 +42,19 @@
 
 AVC_KTIME_DEFINE(fused)   // se_fwd_fused / se_bwd_fused, per precision (avc_ktime.h)
 
+namespace avc {
+// shape-generic kernels: the fragment-count class of a block k stride-2 blocks below an input of
+// class G (an upper bound of its true count: the dead fragments compute on clamped rows, never stored)
+__host__ __device__ constexpr int fz_cls(int G, int k) { return (G >> k) > 0 ? (G >> k) : 1; }
+// the config's blocks subsample as the AdaIN-VC default: 6 blocks, stride 2 on the odd ones
+__device__ __forceinline__ bool fz_std_sub(const FusedArgs& A) {
+    bool s = A.nblk == 6;
+#pragma unroll
+    for (int l = 0; l < 6; ++l) s = s && A.sub[l] == ((l & 1) ? 2 : 1);
+    return s;
+}
+}  // namespace avc
+
 // A-ring depth of the standard-shape kernels' 2-tile GEMMs (the generic shapes keep 4: their
 // step counts are runtime values, and the ring's end-of-GEMM rotation would not fold away)
 #ifndef AVC_FZ_RD_FWD
@@ -418,6 +431,15 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
                   StdSE::Tl(l + 1), StdSE::sub(l));
         });
         TN = StdSE::Tl(StdSE::NBLK);
+    } else if (fz_std_sub(A)) {
+        // the standard subsample pattern at another length: each block on the fragment count of its
+        // own frames (G >> stride-2 blocks before it, at least 1) instead of the input's G -- the deeper
+        // blocks computed 2-8x the fragments they hold (T = 120: se_fwd_fused 126 us against 84 us)
+        static_for<0, 6>([&](auto L) __attribute__((always_inline)) {
+            constexpr int l = decltype(L)::value;
+            block(IC<fz_cls(G, l / 2)>{}, IC<fz_cls(G, (l + 1) / 2)>{}, l, A.Tl[l], A.Tl[l + 1], A.sub[l]);
+        });
+        TN = A.Tl[6];
     } else {
         for (int l = 0; l < A.nblk; ++l)
             block(IC<G>{}, IC<G>{}, l, A.Tl[l], A.Tl[l + 1], A.sub[l]);
@@ -511,7 +533,16 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     KTime* const kt = &g_ktime_fused[KT_FUSED_BWD + (PREC == PREC_BF16)];
     const KtStart kts = ktime_begin(kt);
     const u64* mbase = A.masks + (size_t)b * A.mask_words;
-    auto mwords = [&](int layer) __attribute__((always_inline)) { return mbase + (size_t)(layer * 4 + w) * WPL; };
+    // Shape-generic bf16 kernels read the ReLU' words from an LDS copy of the utterance's set (made once,
+    // below): their K loops have runtime step counts, so the waitcnt pass cannot count the weight-ring loads
+    // issued after a word's global load and waited for it with vmcnt(0) -- draining the next GEMM's ring
+    // at every masked epilogue (T = 120: se_bwd_fused 184 us against 84 us for the standard shape).
+    constexpr bool MLDS = STD == 0 && PREC == PREC_BF16;
+    u64* const MKL = reinterpret_cast<u64*>(fz_lds + fz_lds_bwd(PREC, T));   // (fz_lds_bwd_masks)
+    auto mwords = [&](int layer) __attribute__((always_inline)) {
+        if constexpr (MLDS) return (const u64*)(MKL + (size_t)(layer * 4 + w) * WPL);
+        else return mbase + (size_t)(layer * 4 + w) * WPL;
+    };
 
     // g_pooled, then the first GEMM's weight ring and mask words, are issued before the
     // LDS clearing so their latency hides under it
@@ -543,9 +574,21 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     auto op_c2T = [&](int l) __attribute__((always_inline)) { return aop(A.w.c2T[l], 2 * w, 2, ns_c, ns_c); };
     ARing<2, STD ? AVC_FZ_RD_BWD : 4> ring;
     ring_fill(ring, op_c2T(nblk - 1));
+    if constexpr (MLDS) {   // the utterance's ReLU' words -> LDS: every 16-byte piece in flight at once
+        const int n16 = A.mask_words / 2;                        // (288 words per layer: even)
+        constexpr int MKP = 16;                                  // 64 KB >= the largest set (25 layers: 57.6 KB)
+        const f32x4* src = reinterpret_cast<const f32x4*>(mbase);
+        f32x4* dst = reinterpret_cast<f32x4*>(MKL);
+        f32x4 v[MKP];
+#pragma unroll
+        for (int k = 0; k < MKP; ++k) v[k] = src[min(tid + 256 * k, n16 - 1)];
+#pragma unroll
+        for (int k = 0; k < MKP; ++k)
+            if (tid + 256 * k < n16) dst[tid + 256 * k] = v[k];
+    }
     // ReLU' words of the next layer whose mask is applied, loaded one GEMM ahead
     MaskRd mnext;
-    mnext.load(mwords(nb + 2 + 2 * (nblk - 1)));
+    if constexpr (!MLDS) mnext.load(mwords(nb + 2 + 2 * (nblk - 1)));
 
     char* GB = fz_lds;                          // dilated dY image [T+2ZP] rows
     char* GB2 = GB + (T + 2 * ZP) * RS;         // stride-1 dY image [T+2ZP] rows
@@ -566,6 +609,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
         for (int f = 0; f < NF; ++f) gh[i][f] = (16 * f + c < TN) ? g : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();
+    if constexpr (MLDS) mnext.load(mwords(nb + 2 + 2 * (nblk - 1)));   // (the LDS copy is complete)
     FZ_PH();
 
     int rb[NF];
@@ -670,6 +714,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
             constexpr int l = StdSE::NBLK - 1 - decltype(L)::value;
             constexpr int Ti = StdSE::Tl(l), To = StdSE::Tl(l + 1);
             block(IC<StdSE::nf(To)>{}, IC<StdSE::nf(Ti + 2 * (StdSE::KSZ / 2))>{}, l, Ti, To, StdSE::sub(l));
+        });
+    } else if (fz_std_sub(A)) {   // per-block fragment counts, as in the forward
+        static_for<0, 6>([&](auto L) __attribute__((always_inline)) {
+            constexpr int l = 5 - decltype(L)::value;
+            block(IC<fz_cls(G, (l + 1) / 2)>{}, IC<fz_cls(G, l / 2) + 1>{}, l, A.Tl[l], A.Tl[l + 1], A.sub[l]);
         });
     } else {
         for (int l = A.nblk - 1; l >= 0; --l)
@@ -783,6 +832,9 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     if constexpr (STD != 0) {
         static_for<0, StdSE::NB>([&](auto KB) __attribute__((always_inline)) { bank_bwd(KB); });
     } else {
+        // (a compile-time bank loop here for the default bank at other lengths: 512 VGPRs with 164
+        // spilled in the bf16 instance, se_bwd_fused 176 -> 210 us at T = 120; the fp32 instance
+        // crashes the gfx950 backend)
         for (int kb = 0; kb < nb; ++kb) bank_bwd(kb);
     }
     fold_edges(accx, T, EB, FSCR);

@@ -18,6 +18,11 @@ __host__ __device__ constexpr int fz_lds_bwd_main(int prec, int T) {
 }
 // + per-wave fold scratch [5*16 ch][8 edge columns] fp32
 __host__ __device__ constexpr int fz_lds_bwd(int prec, int T) { return fz_lds_bwd_main(prec, T) + 4 * 5 * 16 * 8 * 4; }
+// launch size: the shape-generic bf16 backward (shape != 0) also holds the utterance's ReLU' words
+// (mask_words u64) after that (avc_fused.hip: MLDS) -- at most 94.7 + 57.6 KB at T = 128
+__host__ __device__ constexpr int fz_lds_bwd_launch(int prec, int T, int shape, int mask_words) {
+    return fz_lds_bwd(prec, T) + (shape != 0 && prec == PREC_BF16 ? 8 * mask_words : 0);
+}
 
 // fused Decoder (avc_vc.hip) at output length Tn: forward = block-input image + conv1
 // output image, (Tn + 2P) rows each; backward = two dY images (Tn + 8 rows) + per-wave

@@ -45,6 +45,17 @@ AVC_KTIME_DEFINE(vc)     // dec_fwd_fused, dec_bwd_fused per precision (avc_ktim
 
 namespace avc {
 
+// shape-generic kernels: the default block structure (6 blocks, x2 upsampling on the even ones) on a
+// content code of at most 16 frames -- block l then holds at most 16 << ((l + 1) / 2) frames, the
+// fragment counts of the standard shape (an upper bound: dead fragments compute on clamped rows and
+// are never stored).  Otherwise every block runs on the kernel's maximum fragment count.
+__device__ __forceinline__ bool dz_std_up(const DecArgs& A) {
+    bool s = A.nblk == 6 && A.Tl[0] <= 16;
+#pragma unroll
+    for (int l = 0; l < 6; ++l) s = s && A.up[l] == ((l & 1) ? 1 : 2);
+    return s;
+}
+
 // the AdaIN-VC decoder at its config.yaml defaults on a 16-frame content code (T = 128)
 struct StdDec {
     static constexpr int T0 = 16, NBLK = 6, KSZ = 5;
@@ -414,7 +425,14 @@ __device__ __forceinline__ void dec_fwd_fused_body(DecArgs A) {
             block(IC<StdDec::nf(StdDec::Tl(l))>{}, l, StdDec::Tl(l), StdDec::up(l));
         });
     } else {
-        for (int l = 0; l < nblk; ++l) block(IC<NF>{}, l, A.Tl[l], A.up[l]);
+        if (dz_std_up(A)) {   // the default upsampling at another length: per-block fragment counts
+            static_for<0, 6>([&](auto L) __attribute__((always_inline)) {
+                constexpr int l = decltype(L)::value;
+                block(IC<(1 << ((l + 1) / 2))>{}, l, A.Tl[l], A.up[l]);
+            });
+        } else {
+            for (int l = 0; l < nblk; ++l) block(IC<NF>{}, l, A.Tl[l], A.up[l]);
+        }
     }
 
     // out_conv (1x1, 128 -> 80) over the Tn frames of HB (rows P + t)
@@ -828,7 +846,14 @@ __device__ __forceinline__ void dec_bwd_fused_body(DecArgs A) {
             block(IC<StdDec::nf(Ti + 2 * (StdDec::KSZ / 2))>{}, l, Ti, StdDec::up(l));
         });
     } else {
-        for (int l = nblk - 1; l >= 0; --l) block(IC<FZ_MAXNF>{}, l, A.Tl[l], A.up[l]);
+        if (dz_std_up(A)) {   // (dec_bwd_fused 250 -> 212 us at T = 120, e2e)
+            static_for<0, 6>([&](auto L) __attribute__((always_inline)) {
+                constexpr int l = 5 - decltype(L)::value;
+                block(IC<(1 << ((l + 1) / 2)) + 1>{}, l, A.Tl[l], A.up[l]);
+            });
+        } else {
+            for (int l = nblk - 1; l >= 0; --l) block(IC<FZ_MAXNF>{}, l, A.Tl[l], A.up[l]);
+        }
     }
     FZ_PH();
     FZ_PH_DUMP("dbwd");
