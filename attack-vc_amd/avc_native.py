@@ -93,6 +93,9 @@ SIGNATURES = [
     ("avc_sn_state_count", ctypes.c_size_t, [ctypes.c_void_p]),
     ("avc_set_sn_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("avc_get_sn_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("avc_sn_state_dev", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.c_void_p]),
+    ("avc_set_sn_train", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     ("avc_content_encoder", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("avc_content_frames", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -363,24 +366,35 @@ class Context:
 
     def _sn_call(self, fn):
         """Run fn() (a call that runs Decoder forwards) with a spectral-norm Decoder's u / v loaded
-        from its module buffers and written back afterwards, as the reference's train-mode
-        spectral_norm hook updates them (models.py:382)."""
+        from its module buffers, under the hook mode the module's .training selects (torch's
+        spectral_norm compute_weight, models.py:382):
+          train: one power iteration per Decoder forward, the buffers written back afterwards (the
+                 reference never calls .eval(), so its attacks run this mode);
+          eval : sigma = u . (W v) from the stored u / v, the buffers left as they are.
+        Device buffers are copied device-to-device on the caller's stream (no host round trip)."""
         dec = self._sn_dec() if self._sn_dec is not None else None
         if dec is None:
             return fn()
         bufs = _sn_buffers(dec)
-        uv = torch.cat([b.detach().reshape(-1).to("cpu", torch.float32) for b in bufs]).contiguous()
         n = lib().avc_sn_state_count(self.h)
+        train = bool(dec.training)
+        on_dev = all(b.is_cuda for b in bufs)
+        dev = bufs[0].device if on_dev else torch.device("cuda", torch.cuda.current_device())
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        with torch.no_grad():
+            uv = torch.cat([b.detach().reshape(-1).to(dev, torch.float32) for b in bufs]).contiguous()
         if uv.numel() != n:
             raise RuntimeError(f"spectral-norm state: module holds {uv.numel()} u / v values, libavc expects {n}")
-        _check(lib().avc_set_sn_state(self.h, ctypes.c_void_p(uv.data_ptr()), n))
+        _check(lib().avc_set_sn_train(self.h, int(train), stream))
+        _check(lib().avc_sn_state_dev(self.h, ctypes.c_void_p(uv.data_ptr()), n, 1, stream))
         out = fn()
-        _check(lib().avc_get_sn_state(self.h, ctypes.c_void_p(uv.data_ptr()), n))
-        with torch.no_grad():
-            o = 0
-            for b in bufs:
-                b.copy_(uv[o:o + b.numel()].view_as(b))
-                o += b.numel()
+        if train:
+            _check(lib().avc_sn_state_dev(self.h, ctypes.c_void_p(uv.data_ptr()), n, 0, stream))
+            with torch.no_grad():
+                o = 0
+                for b in bufs:
+                    b.copy_(uv[o:o + b.numel()].view_as(b))
+                    o += b.numel()
         return out
 
     def vc_out_frames(self, T: int) -> int:

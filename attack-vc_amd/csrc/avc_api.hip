@@ -1834,7 +1834,9 @@ extern "C" avc::KTime* avc_ktime_records_vc();
 extern "C" int avc_ktime(avc_ctx* ctx, int enable, double* avg_us, int64_t* launches) {
     if (!ctx) return fail("avc_ktime: null context");
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // the records are per device, shared by every context and stream on it: drain the whole device, so no
+    // stamped kernel of another context can race the read-out / reset below
+    HIPCHK(hipDeviceSynchronize());
     avc::KTime* units[3] = {avc_ktime_records_fused(), avc_ktime_records_long(), avc_ktime_records_vc()};
     const int used[3] = {4, 8, 4};   // records in use per unit (avc_ktime.h slots), in avc_ktime's output order
     int rate_khz = 0;

@@ -288,6 +288,8 @@ struct SnArgs {
     float* uv;
     float* sigma;                     // [layers]
     const SnChunk* chunks;
+    const int* train;                 // device flag: 1 = train-mode hook (power iteration, u / v updated),
+                                      // 0 = eval mode (sigma = u.(W v) from the stored u / v, nothing written)
 };
 
 // VSMask PredictiveModel layer (avc_pm.hip): implicit GEMM over NCHW activations.

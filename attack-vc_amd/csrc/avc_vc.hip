@@ -1093,6 +1093,25 @@ __global__ void __launch_bounds__(256) sn_power(SnArgs A) {
     float* u = A.uv + L.u_off;
     float* v = A.uv + L.v_off;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (*A.train == 0) {
+        // eval mode (torch's compute_weight with do_power_iteration = False): sigma = u . (W v) from the
+        // stored u / v, which stay as they are
+        for (int j = tid; j < L.w; j += 256) sv[j] = v[j];
+        __syncthreads();
+        float sg = 0.f;
+        for (int i = wv; i < L.h; i += 4) {
+            float s = 0.f;
+            for (int j = lane; j < L.w; j += 64) s = __builtin_fmaf(W[(size_t)i * L.w + j], sv[j], s);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+            if (lane == 0) su[i] = s;
+        }
+        __syncthreads();
+        for (int i = tid; i < L.h; i += 256) sg = __builtin_fmaf(u[i], su[i], sg);
+        const float sigma = sn_block_sum(sg, red);
+        if (tid == 0) A.sigma[blockIdx.x] = sigma;
+        return;
+    }
     for (int i = tid; i < L.h; i += 256) su[i] = u[i];
     __syncthreads();
     // v = normalize(W^T u): one column per thread (coalesced rows of W), rows in order

@@ -88,14 +88,47 @@ def parse():
     return ap.parse_args()
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def visible_gpu_count(nodes=KFD_NODES, dev_dir="/dev/dri") -> int:
+    """GPUs this process can open, counted WITHOUT initialising HIP (launch_ranks must not: a process
+    that has initialised the GPU may not fork the rank processes): the KFD topology nodes with a non-zero
+    gpu_id whose DRM render node exists and is accessible, narrowed by ROCR_VISIBLE_DEVICES /
+    HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES as the runtime applies them.  Never calls into torch.cuda
+    (torch's device_count falls back to hipGetDeviceCount when amdsmi is unavailable)."""
+    n = 0
+    try:
+        names = sorted(os.listdir(nodes))
+    except OSError:
+        names = []
+    for d in names:
+        try:
+            with open(os.path.join(nodes, d, "properties")) as fh:
+                props = dict(ln.split(None, 1) for ln in fh.read().splitlines() if len(ln.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("gpu_id", "0").strip() or 0) == 0:
+            continue                      # a CPU node
+        minor = props.get("drm_render_minor", "").strip()
+        if minor and not os.access(os.path.join(dev_dir, f"renderD{minor}"), os.R_OK | os.W_OK):
+            continue                      # listed by the host's topology, not passed to this container
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(a) -> int:
     """--gpus N without torchrun: start N rank processes of this script (RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* set like torchrun, 127.0.0.1 rendezvous) and return the worst exit
-    code.  Runs before anything touches the GPU in this process (device_count() does not)."""
+    code.  Nothing in this process touches the GPU: the count comes from sysfs (visible_gpu_count)."""
     import socket
     import subprocess
     if not a.dry_run:
-        n = torch.cuda.device_count()
+        n = visible_gpu_count()
         if n < a.gpus:
             raise SystemExit(f"bench.py: --gpus {a.gpus} requested but only {n} GPU(s) are visible; "
                              f"refusing to report a {n}-GPU number as {a.gpus}")

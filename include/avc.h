@@ -60,7 +60,9 @@ typedef struct avc_se_cfg {
     int32_t act;
 } avc_se_cfg;
 
-/* Arithmetic of the per-iteration loop. FP32: exact-f32 MFMA (v_mfma_f32_32x32x2_f32). */
+/* Arithmetic of the per-iteration loop.  FP32: exact-f32 MFMA (v_mfma_f32_16x16x4_f32 in the fused /
+ * long engines, avc_fused_core.h); BF16: v_mfma_f32_16x16x32_bf16 operands, fp32 accumulation,
+ * fp32 InstanceNorm statistics, loss and Adam state. */
 enum { AVC_PREC_FP32 = 0, AVC_PREC_BF16 = 1 };
 
 /* Loss reduction over a batch of B utterances.
@@ -166,6 +168,14 @@ int avc_attach_vc(avc_ctx* ctx, const avc_vc_cfg* cfg, const float* weights, siz
 size_t avc_sn_state_count(avc_ctx* ctx);
 int avc_set_sn_state(avc_ctx* ctx, const float* uv, size_t n);
 int avc_get_sn_state(avc_ctx* ctx, float* uv, size_t n);
+/* The same state as a DEVICE buffer of avc_sn_state_count floats, copied on `stream` (ordered with
+ * the caller's other work on it, no synchronisation): set = 1 loads it, set = 0 stores it. */
+int avc_sn_state_dev(avc_ctx* ctx, float* uv, size_t n, int set, void* stream);
+/* The hook's mode, as the Decoder module's .training says (torch spectral_norm.py compute_weight):
+ *   train = 1 (default): one power iteration per forward, u / v updated;
+ *   train = 0 (eval)   : sigma = u . (W v) from the stored u / v, which stay unchanged.
+ * Ordered on `stream` like the calls that follow it. */
+int avc_set_sn_train(avc_ctx* ctx, int train, void* stream);
 
 /* Frames of the Decoder output for T input frames (T -> ContentEncoder length -> x upsample). */
 int avc_vc_out_frames(avc_ctx* ctx, int T);

@@ -279,11 +279,16 @@ def spectral_norm_step(w, p="decoder."):
     Decoder layer that has a weight_orig: one power iteration on W = weight_orig.reshape(out, -1),
         v = normalize(W^T u),  u = normalize(W v)   (normalize: x / max(||x||, 1e-12)),
         sigma = u . (W v),     weight = weight_orig / sigma,
-    with u, v updated in place (the module buffers weight_u / weight_v).  No-op for sn=False."""
+    with u, v updated in place (the module buffers weight_u / weight_v).  No-op for sn=False.
+    w.sn_train = False: the eval-mode hook (compute_weight with do_power_iteration=False) --
+    sigma = u . (W v) from the stored u / v, which stay unchanged."""
     for k in [k for k in w.d if k.startswith(p) and k.endswith(".weight_orig")]:
         n = k[: -len("weight_orig")]
         W = w.d[k]
         Wm = W.reshape(W.shape[0], -1)
+        if not getattr(w, "sn_train", True):
+            w.d[n + "weight"] = W / (w.d[n + "weight_u"] @ (Wm @ w.d[n + "weight_v"]))
+            continue
         eps = W.dtype.type(1e-12)
         v = Wm.T @ w.d[n + "weight_u"]
         v = v / max(np.sqrt((v * v).sum()), eps)

@@ -10,6 +10,10 @@ cycles summed over every SIMD of the chip over the SIMD-cycles the dispatch last
 in [0, 1] by construction and independent of the clock.  HBM bytes = 2 x FETCH_SIZE +
 WRITE_SIZE (KiB; gfx950 FETCH_SIZE counts half of wide reads, MI355X_MICROARCH.md).
 The first --warm dispatches of every kernel (graph capture, cold caches) are skipped.
+Round 6: for a short kernel GRBM_GUI_ACTIVE spans more than the dispatch (the counter window's
+set-up and drain), which gave "clocks" above the 2.4 GHz maximum; the SIMD-cycles of a dispatch are
+therefore min(GRBM_GUI_ACTIVE / 8, trace duration x 2.4 GHz) -- capped rows are marked with * and
+their MFMA util is the trace-duration figure (a lower bound if the clock ran below 2.4 GHz).
 """
 import argparse
 import csv
@@ -21,6 +25,7 @@ import statistics
 from collections import defaultdict
 
 SIMDS = 1024
+CLK_MAX = 2.4     # GHz, MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def short(name):
@@ -104,6 +109,9 @@ def main():
         us = statistics.median(dur[k])
         gui = c.get("GRBM_GUI_ACTIVE")
         cyc = gui / 8 if gui else None
+        capped = cyc is not None and cyc > us * 1e3 * CLK_MAX
+        if capped:
+            cyc = us * 1e3 * CLK_MAX
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
         util = busy / (SIMDS * cyc) if busy is not None and cyc else None
         hbm = None
@@ -116,7 +124,8 @@ def main():
         mf_per = c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["SQ_INSTS_MFMA"] if c.get("SQ_INSTS_MFMA") and busy else None
         d = {"launches": len(dur[k]) + a.warm, "median_us": round(us, 2), "mfma_util": util, "hbm_bytes": hbm,
              "hbm_GBps": hbm / (us * 1e3) if hbm else None, "clock_GHz": clk, "wave_state": split,
-             "lds_conflict_cycles_per_lds_cycle": lds_conf, "mfma_busy_per_inst": mf_per, "counters": c}
+             "lds_conflict_cycles_per_lds_cycle": lds_conf, "mfma_busy_per_inst": mf_per, "counters": c,
+             "cycles_capped_to_trace": capped}
         out_json[k] = d
         rows.append((k, d))
     lines = ["| kernel | median µs | MFMA util | HBM MB | HBM GB/s | clock GHz | wait / inst-stall / active | LDS conflict |",
@@ -127,7 +136,7 @@ def main():
         wsf = " / ".join(f(ws.get(n), 2) for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"))
         lines.append(f"| {k} | {d['median_us']} | {f(d['mfma_util'])} | "
                      f"{f(d['hbm_bytes'] / 1e6 if d['hbm_bytes'] else None, 1)} | {f(d['hbm_GBps'], 0)} | "
-                     f"{f(d['clock_GHz'], 2)} | {wsf} | {f(d['lds_conflict_cycles_per_lds_cycle'])} |")
+                     f"{f(d['clock_GHz'], 2)}{'*' if d['cycles_capped_to_trace'] else ''} | {wsf} | {f(d['lds_conflict_cycles_per_lds_cycle'])} |")
     txt = "\n".join(lines)
     print(txt)
     if a.out:
@@ -135,7 +144,8 @@ def main():
         with open(a.out + "_summary.md", "w") as fh:
             fh.write(f"# {os.path.basename(a.out)}\n\nlibavc src={src}.  Source: `{a.dir}` (rocprofv3 kernel trace + PMC passes of "
                      f"avc_bench; first {a.warm} dispatches per kernel skipped).  MFMA util = "
-                     "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8).  HBM = 2 x FETCH_SIZE + "
+                     "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x min(GRBM_GUI_ACTIVE/8, trace duration x 2.4 GHz)); * = the "
+                     "counter window outlasted the dispatch, cycles taken from the trace duration.  HBM = 2 x FETCH_SIZE + "
                      "WRITE_SIZE.  Wave state = fractions of SQ_WAVE_CYCLES.\n\n" + txt + "\n")
         json.dump(out_json, open(a.out + "_counters.json", "w"), indent=1)
         st = glob.glob(os.path.join(a.dir, "trace", "**", "*kernel_stats.csv"), recursive=True)

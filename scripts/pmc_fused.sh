@@ -7,6 +7,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# no in-graph kernel stamps: their closing atomics lengthen every launch by ~9 us
+export AVC_BENCH_KTIME=0
 P=${PREC:-1}
 A=${ATTACK:-0}
 ITERS=${ITERS:-20}

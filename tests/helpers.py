@@ -43,8 +43,10 @@ TOL_VC_GRAD_L2_MEDIAN = 2e-5
 # float64 vs the golden; 5.5e-8 for the oracle's fp32), so an independent fp32 evaluation can sit ~2x that
 # from the golden (measured 1.37e-7 once every engine computes vc + eps * tanh(ptb) unfused, as the
 # reference does).
+# Round 6: 2e-7 applies to the e2e / fb chains only (TOL_ADV_MEAN_VC); the emb attack keeps 1e-7.
 TOL_ADV = {1: 1e-6, 10: 5e-5, 100: 1e-4, 1500: 5e-4}
-TOL_ADV_MEAN = {1: 1e-8, 10: 2e-7, 100: 1e-6, 1500: 5e-6}
+TOL_ADV_MEAN = {1: 1e-8, 10: 1e-7, 100: 1e-6, 1500: 5e-6}
+TOL_ADV_MEAN_VC = {**TOL_ADV_MEAN, 10: 2e-7}
 
 
 def check_grad_flip_robust(g, ref, frac=0.05):
@@ -63,7 +65,9 @@ def check_grad_flip_robust(g, ref, frac=0.05):
     assert off.mean() <= frac, off.mean()
 
 
-def check_adv(adv, ref, n):
+def check_adv(adv, ref, n, kind="emb"):
+    """adv vs a reference adv after n iterations; kind "e2e" / "fb" (the chain through the Decoder) takes
+    the VC mean bound at n = 10."""
     d = np.abs(np.asarray(adv, np.float64) - np.asarray(ref, np.float64))
     log = os.environ.get("AVC_TOL_LOG")
     if log:   # calibration runs: record every comparison (scripts/tol_calibration.py)
@@ -73,7 +77,8 @@ def check_adv(adv, ref, n):
             fh.write(json.dumps({"n": n, "max": float(d.max()), "mean": float(d.mean()),
                                  "where": f"{os.path.basename(caller.filename)}:{caller.function}"}) + "\n")
     assert d.max() <= TOL_ADV[n], (n, d.max())
-    assert d.mean() <= TOL_ADV_MEAN[n], (n, d.mean())
+    mean_tol = (TOL_ADV_MEAN_VC if kind in ("e2e", "fb") else TOL_ADV_MEAN)[n]
+    assert d.mean() <= mean_tol, (n, kind, d.mean())
 
 
 def cfg_of(z):

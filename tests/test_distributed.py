@@ -117,3 +117,43 @@ def test_bench_refuses_missing_gpus():
     r = _bench("--gpus", "2", "--steps", "1", timeout=120)
     assert r.returncode != 0
     assert "GPU(s) are visible" in (r.stderr + r.stdout)
+
+
+def test_launcher_gpu_count_never_initialises_hip(tmp_path, monkeypatch):
+    """bench.py's launcher counts GPUs from sysfs (KFD topology + accessible render nodes, narrowed by the
+    *_VISIBLE_DEVICES variables) and never calls into torch.cuda: a process that has initialised HIP must
+    not fork the rank processes."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    def boom(*a, **k):
+        raise AssertionError("the launcher's GPU count reached torch.cuda / HIP")
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom, raising=False)
+    monkeypatch.setattr(torch.cuda, "is_available", boom)
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    nodes, dri = tmp_path / "nodes", tmp_path / "dri"
+    nodes.mkdir()
+    dri.mkdir()
+    # node 0: a CPU; nodes 1-3: GPUs with render minors 128-130, of which 130 is not in this "container"
+    for i, (gid, minor) in enumerate([(0, None), (1111, 128), (2222, 129), (3333, 130)]):
+        (nodes / str(i)).mkdir()
+        txt = f"cpu_cores_count 8\ngpu_id {gid}\n" + (f"drm_render_minor {minor}\n" if minor else "")
+        (nodes / str(i) / "properties").write_text(txt)
+    for minor in (128, 129):
+        (dri / f"renderD{minor}").write_text("")
+    assert bench.visible_gpu_count(str(nodes), str(dri)) == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert bench.visible_gpu_count(str(nodes), str(dri)) == 1
+    assert bench.visible_gpu_count(str(tmp_path / "absent"), str(dri)) == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    # the launcher refuses more ranks than visible GPUs, through the same count
+    monkeypatch.setattr(bench, "KFD_NODES", str(tmp_path / "absent"))
+    monkeypatch.setattr(bench, "visible_gpu_count", lambda nodes=None, dev_dir=None: 0)
+
+    class A:
+        dry_run, gpus = False, 2
+    with pytest.raises(SystemExit, match="only 0 GPU"):
+        bench.launch_ranks(A())

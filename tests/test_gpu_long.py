@@ -158,7 +158,7 @@ def test_long_vc_golden_T300(full, golden, kind):
     fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
     adv, info = fn(m, _dev(zl["vc_src"]), _dev(zl["vc_tgt"]), _dev(zl["adv_tgt"]), 0.1, 10,
                    ptb0=_dev(zl[f"{kind}_ptb0"]), return_info=True)
-    check_adv(adv.detach().cpu().numpy(), zl[f"{kind}_adv_n10"], 10)
+    check_adv(adv.detach().cpu().numpy(), zl[f"{kind}_adv_n10"], 10, kind=kind)
     assert rel(info["grad0"].cpu().numpy(), zl[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
     np.testing.assert_allclose(info["losses"].cpu().numpy().T, zl[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
 
@@ -175,7 +175,7 @@ def test_long_golden_T300_n100(full, golden, kind):
     args = (_dev(zl["vc_tgt"]), _dev(zl["adv_tgt"])) if kind == "emb" else \
         (_dev(zl["vc_src"]), _dev(zl["vc_tgt"]), _dev(zl["adv_tgt"]))
     adv, info = fn(m, *args, 0.1, 100, ptb0=_dev(zn[f"{kind}_ptb0"]), return_info=True)
-    check_adv(adv.detach().cpu().numpy(), zn[f"{kind}_adv_n100"], 100)
+    check_adv(adv.detach().cpu().numpy(), zn[f"{kind}_adv_n100"], 100, kind=kind)
     assert rel(info["grad0"].cpu().numpy(), zn[f"{kind}_grad0"]) <= (TOL_GRAD_REL if kind == "emb" else TOL_GRAD_REL_VC)
     np.testing.assert_allclose(info["losses"].cpu().numpy().T, zn[f"{kind}_losses_n100"], rtol=2e-4, atol=1e-9)
 

@@ -44,7 +44,7 @@ def test_lrelu_attacks(lrelu, kind):
     else:
         fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
         adv, info = fn(m, t["vc_src"], t["vc_tgt"], t["adv_tgt"], 0.1, 10, ptb0=t[f"{kind}_ptb0"], return_info=True)
-    check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10)
+    check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10, kind=kind)
     g = info["grad0"].cpu().numpy()
     if kind == "emb":
         assert rel(g, z[f"{kind}_grad0"]) <= TOL_GRAD_REL

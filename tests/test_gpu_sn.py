@@ -58,7 +58,7 @@ def test_sn_attack_golden(sn, kind):
     m = copy.deepcopy(m0).to(DEV)
     adv, info = FN[kind](m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
                          ptb0=_dev(z[f"{kind}_ptb0"]), return_info=True)
-    check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10)
+    check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10, kind=kind)
     assert rel(info["grad0"].cpu().numpy(), z[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
     np.testing.assert_allclose(info["losses"].cpu().numpy().T, z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
     assert _uv_err(m, z, f"uv_{kind}") <= 1e-5
@@ -91,3 +91,36 @@ def test_sn_bf16_and_state_carries_over(sn, kind):
     assert torch.equal(b1, b3), float((b1 - b3).abs().max())
     for k, v in m3.decoder.state_dict().items():          # and both leave the same u / v
         assert torch.equal(v, m1.decoder.state_dict()[k]), k
+
+
+def test_sn_eval_mode(golden):
+    """After .eval() (tests/golden/make_sn_eval.py, the real reference in eval mode): no power iteration,
+    sigma = u . (W v) from the stored u / v, the buffers untouched -- inference at the initial and at a
+    moved u / v, and the e2e attack at n = 10 against the reference's adv."""
+    z = golden("full_sn_eval_T128")
+    m0 = model_from_fixture(z)
+    m = copy.deepcopy(m0).to(DEV).eval()
+    before = {k: v.clone() for k, v in m.decoder.state_dict().items()}
+    out = m.inference(_dev(z["vc_src"]), _dev(z["vc_tgt"])).cpu().numpy()
+    assert rel(out, z["inference_eval"]) <= 1e-4, rel(out, z["inference_eval"])
+    out2 = m.inference(_dev(z["vc_src"]), _dev(z["vc_tgt"])).cpu().numpy()
+    assert np.array_equal(out, out2)                       # no state moved between the calls
+    for k, v in m.decoder.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    with torch.no_grad():
+        for k in z:
+            if k.startswith("uv1/"):
+                m.decoder.state_dict()[k.split("/", 1)[1]].copy_(_dev(z[k]))
+    out = m.inference(_dev(z["vc_src"]), _dev(z["vc_tgt"])).cpu().numpy()
+    assert rel(out, z["inference_eval_uv1"]) <= 1e-4, rel(out, z["inference_eval_uv1"])
+    m = copy.deepcopy(m0).to(DEV).eval()
+    adv = attack_utils.e2e_attack(m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
+                                  ptb0=_dev(z["e2e_ptb0_eval"]))
+    check_adv(adv.detach().cpu().numpy(), z["e2e_adv_n10_eval"], 10, kind="e2e")
+    for k, v in m.decoder.state_dict().items():
+        assert torch.equal(v.cpu(), m0.decoder.state_dict()[k].cpu()), k
+    # and back in train mode the hook iterates again (the buffers move)
+    m.train()
+    m.inference(_dev(z["vc_src"]), _dev(z["vc_tgt"]))
+    assert any(not torch.equal(v.cpu(), m0.decoder.state_dict()[k].cpu())
+               for k, v in m.decoder.state_dict().items() if k.endswith(("_u", "_v")))

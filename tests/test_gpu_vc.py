@@ -46,7 +46,7 @@ def test_vc_attack_golden(full, kind):
     fn = attack_utils.e2e_attack if kind == "e2e" else attack_utils.fb_attack
     adv, info = fn(m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
                    ptb0=_dev(z[f"{kind}_ptb0"]), return_info=True)
-    check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10)
+    check_adv(adv.detach().cpu().numpy(), z[f"{kind}_adv_n10"], 10, kind=kind)
     assert rel(info["grad0"].cpu().numpy(), z[f"{kind}_grad0"]) <= (TOL_GRAD_REL_VC if kind != "emb" else TOL_GRAD_REL)
     np.testing.assert_allclose(info["losses"].cpu().numpy().T, z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
 

@@ -44,7 +44,7 @@ def test_vc_attack_golden_n100(full, golden, kind):
     zn = golden("full_T128_n100")
     adv, info = FN[kind](m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 100,
                          ptb0=_dev(zn[f"{kind}_ptb0"]), return_info=True)
-    check_adv(adv.detach().cpu().numpy(), zn[f"{kind}_adv_n100"], 100)
+    check_adv(adv.detach().cpu().numpy(), zn[f"{kind}_adv_n100"], 100, kind=kind)
     assert rel(info["grad0"].cpu().numpy(), zn[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
     np.testing.assert_allclose(info["losses"].cpu().numpy().T, zn[f"{kind}_losses_n100"], rtol=2e-4, atol=1e-9)
 

@@ -127,7 +127,7 @@ def test_vc_attacks(golden, name, kind):
     rec = {}
     adv = getattr(oracle, f"{kind}_attack")(w, cfg_of(z), z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 10,
                                             z[f"{kind}_ptb0"], record=rec)
-    check_adv(adv, z[f"{kind}_adv_n10"], 10)
+    check_adv(adv, z[f"{kind}_adv_n10"], 10, kind=kind)
     assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= (TOL_GRAD_REL_VC if kind != "emb" else TOL_GRAD_REL)
     np.testing.assert_allclose(rec["losses"], z[f"{kind}_losses_n10"], rtol=1e-4, atol=1e-9)
 
@@ -143,7 +143,7 @@ def test_vc_attacks_full_n100(golden, kind):
     rec = {}
     adv = getattr(oracle, f"{kind}_attack")(w, cfg_of(z), z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 100,
                                             zn[f"{kind}_ptb0"], record=rec)
-    check_adv(adv, zn[f"{kind}_adv_n100"], 100)
+    check_adv(adv, zn[f"{kind}_adv_n100"], 100, kind=kind)
     assert rel(rec["grad0"], zn[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
     np.testing.assert_allclose(rec["losses"], zn[f"{kind}_losses_n100"], rtol=2e-4, atol=1e-9)
 
@@ -183,7 +183,7 @@ def test_torch_cpu_vc_baseline_matches_reference(golden, kind):
     sd = model_from_fixture(z).state_dict()
     out = torch_cpu.vc_attack(kind, sd, cfg_of(z), torch.from_numpy(z["vc_src"][:1]), torch.from_numpy(z["vc_tgt"][:1]),
                               torch.from_numpy(z["adv_tgt"][:1]), 0.1, 10, torch.from_numpy(z[f"{kind}_ptb0"][:1]))
-    check_adv(out.numpy(), z[f"{kind}_adv_n10"][:1], 10)
+    check_adv(out.numpy(), z[f"{kind}_adv_n10"][:1], 10, kind=kind)
 
 
 def test_predictive_model_oracle_and_init(golden):
@@ -235,7 +235,7 @@ def test_lrelu_config(golden, kind):
         assert rel(oracle.inference(w, cfg, z["vc_src"], z["vc_tgt"]), z["inference"]) <= 1e-5
     rec = {}
     adv = oracle.attack(kind, w, cfg, z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 10, z[f"{kind}_ptb0"], record=rec)
-    check_adv(adv, z[f"{kind}_adv_n10"], 10)
+    check_adv(adv, z[f"{kind}_adv_n10"], 10, kind=kind)
     assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= (TOL_GRAD_REL_VC if kind != "emb" else TOL_GRAD_REL)
 
 
@@ -256,7 +256,7 @@ def test_long_mixed_lengths_fixture(golden):
         fn = getattr(oracle, f"{kind}_attack")
         args = (z["vc_tgt"], z["adv_tgt"]) if kind == "emb" else (z["vc_src"], z["vc_tgt"], z["adv_tgt"])
         adv = fn(w, cfg, *args, 0.1, 10, z[f"{kind}_ptb0"], record=rec)
-        check_adv(adv, z[f"{kind}_adv_n10"], 10)
+        check_adv(adv, z[f"{kind}_adv_n10"], 10, kind=kind)
         assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= (TOL_GRAD_REL if kind == "emb" else TOL_GRAD_REL_VC)
         np.testing.assert_allclose(rec["losses"], z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
 
@@ -358,7 +358,33 @@ def test_spectral_norm_decoder_oracle(golden):
     for kind in ("e2e", "fb"):
         w, rec = oracle.Weights(sd), {}
         adv = oracle.attack(kind, w, cfg, z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 10, z[f"{kind}_ptb0"], record=rec)
-        check_adv(adv, z[f"{kind}_adv_n10"], 10)
+        check_adv(adv, z[f"{kind}_adv_n10"], 10, kind=kind)
         assert rel(rec["grad0"], z[f"{kind}_grad0"]) <= TOL_GRAD_REL_VC
         np.testing.assert_allclose(rec["losses"], z[f"{kind}_losses_n10"], rtol=2e-4, atol=1e-9)
         assert uv_err(w, f"uv_{kind}") <= 1e-6        # 1 (fb) / 2 (e2e) precompute forwards + 10 iterations
+
+
+def test_spectral_norm_eval_oracle(golden):
+    """The eval-mode hook (tests/golden/make_sn_eval.py, the real reference after .eval()): no power
+    iteration, sigma from the stored u / v -- inference at the initial and at a moved u / v, and the e2e
+    attack at n = 10 (the Decoder's weights then fixed); the buffers never change."""
+    z = golden("full_sn_eval_T128")
+    m = model_from_fixture(z)
+    sd = {k: v.detach().numpy() for k, v in m.state_dict().items()}
+    cfg = cfg_of(z)
+    w = oracle.Weights(dict(sd))
+    w.sn_train = False
+    u0 = {k: v.copy() for k, v in w.d.items() if k.endswith(("_u", "_v"))}
+    assert rel(oracle.inference(w, cfg, z["vc_src"], z["vc_tgt"]), z["inference_eval"]) <= 1e-5
+    for k, v in u0.items():
+        assert np.array_equal(w.d[k], v), k
+    w1 = oracle.Weights(dict(sd))
+    w1.sn_train = False
+    for k in z:
+        if k.startswith("uv1/"):
+            w1.d["decoder." + k.split("/", 1)[1]] = z[k]
+    assert rel(oracle.inference(w1, cfg, z["vc_src"], z["vc_tgt"]), z["inference_eval_uv1"]) <= 1e-5
+    w = oracle.Weights(dict(sd))
+    w.sn_train = False
+    adv = oracle.attack("e2e", w, cfg, z["vc_src"], z["vc_tgt"], z["adv_tgt"], 0.1, 10, z["e2e_ptb0_eval"])
+    check_adv(adv, z["e2e_adv_n10_eval"], 10, kind="e2e")
