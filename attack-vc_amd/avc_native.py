@@ -78,6 +78,10 @@ SIGNATURES = [
     ("avc_emb_attack_emb", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                           ctypes.c_void_p, ctypes.POINTER(AttackOpts), ctypes.c_void_p]),
+    ("avc_emb_attack_ragged", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                             ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(AttackOpts),
+                                             ctypes.c_void_p]),
     ("avc_header_optimize", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                            ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
@@ -312,6 +316,49 @@ class Context:
                                                 B, T, float(eps), int(n_iters), ctypes.c_void_p(out.data_ptr()),
                                                 ctypes.byref(o), ctypes.c_void_p(stream)))
         return out, losses, grad0
+
+    def emb_attack_ragged(self, vc_tgts, tgt_emb, ptb0s, eps: float, n_iters: int, precision="fp32",
+                          use_graph=True, want_losses=False, want_grad0=False, update="adam", pgd_step=1e-3):
+        """avc_emb_attack_ragged: ONE batch of utterances of different lengths (vc_tgts[b] [80, T_b], ptb0s[b]
+        likewise; tgt_emb [B, c_out] = SpeakerEncoder(adv_tgt_b), each embedded at its own length) -- every
+        pass is one launch over all of them (the long engine with per-workgroup lengths).  Returns
+        (adv list [80, T_b], losses [n_iters, B] or None, grad0 list or None)."""
+        B = len(vc_tgts)
+        if B == 0 or len(ptb0s) != B:
+            raise RuntimeError("emb_attack_ragged: one ptb0 per utterance, at least one utterance")
+        c_in = self.cfg["c_in"]
+        for name, ts in (("vc_tgt", vc_tgts), ("ptb0", ptb0s)):
+            for b, t in enumerate(ts):
+                _require_gpu(t)
+                if t.dim() != 2 or t.shape[0] != c_in:
+                    raise RuntimeError(f"{name}[{b}]: expected [{c_in}, T], got {tuple(t.shape)}")
+        lens = [int(t.shape[1]) for t in vc_tgts]
+        if [int(t.shape[1]) for t in ptb0s] != lens:
+            raise RuntimeError("emb_attack_ragged: ptb0 lengths differ from vc_tgt lengths")
+        dev = vc_tgts[0].device
+        vc = torch.cat([t.reshape(-1).float() for t in vc_tgts]).contiguous()
+        p0 = torch.cat([t.reshape(-1).float() for t in ptb0s]).to(dev).contiguous()
+        tgt_emb = self._tgt_emb(tgt_emb, B)
+        out = torch.empty_like(vc)
+        o, losses, g0 = self._opts(precision, "independent", use_graph, n_iters, torch.empty(B, 1, device=dev),
+                                   want_losses, False, update, pgd_step)
+        grad0 = torch.empty_like(vc) if want_grad0 and n_iters > 0 else None
+        if grad0 is not None:
+            o.grad0 = grad0.data_ptr()
+        arr = (ctypes.c_int * B)(*lens)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        with self._lock:
+            _check(lib().avc_emb_attack_ragged(self.h, ctypes.c_void_p(vc.data_ptr()), arr, B,
+                                               ctypes.c_void_p(tgt_emb.data_ptr()), ctypes.c_void_p(p0.data_ptr()),
+                                               float(eps), int(n_iters), ctypes.c_void_p(out.data_ptr()),
+                                               ctypes.byref(o), ctypes.c_void_p(stream)))
+        def split(x):
+            res, off = [], 0
+            for T in lens:
+                res.append(x[off:off + c_in * T].view(c_in, T))
+                off += c_in * T
+            return res
+        return split(out), losses, (split(grad0) if grad0 is not None else None)
 
     def header_optimize(self, source, target, header, n_iters: int, epsilon=0.1, lambda_param=0.5, lr=1e-3,
                         betas=(0.9, 0.999), adam_eps=1e-8, precision="fp32", adam_state=None):

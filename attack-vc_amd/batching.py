@@ -17,7 +17,16 @@ batch.  `attack_many` therefore
 
 Every chunk runs the same per-utterance arithmetic as a single-utterance call (the kernels are
 batch-invariant, tests/test_gpu_parity.py::test_batch_shard_invariance), so utterance i of the
-result equals attack_utils.*_attack on utterance i alone, bit for bit.  libavc caches one
+result equals attack_utils.*_attack on utterance i alone, bit for bit.
+
+ragged=True (emb attack): instead of one batch per length, ONE ragged batch per chunk of up to
+max_batch utterances of ANY lengths (avc_emb_attack_ragged: every SpeakerEncoder pass is one launch,
+each workgroup its own utterance length, on the long engine), longest first so that neighbouring
+workgroups -- dealt round-robin over the 8 XCDs -- carry similar work.  With real data's spread of
+lengths the per-length buckets are mostly of one or two utterances (a handful of the 256 CUs busy);
+the ragged batch keeps every CU busy.  Utterance i then equals its single-utterance attack on the long
+engine (AVC_ENGINE_LONG) bit for bit -- the fused engine's result too in fp32, where the two engines
+are bitwise equal (tests/test_gpu_long.py).  libavc caches one
 workspace (buffers, plans, captured graphs) per shape, and attack_many sizes that cache to the
 shapes it uses, so a second call over the same lengths re-plans nothing (avc_ws_stats).
 """
@@ -67,7 +76,7 @@ def _mel(name: str, t: torch.Tensor) -> torch.Tensor:
 def attack_many(kind: str, model_per_device: Sequence[torch.nn.Module], vc_tgts: Sequence[torch.Tensor],
                 adv_tgts: Sequence[torch.Tensor], eps: float, n_iters: int,
                 vc_srcs: Optional[Sequence[torch.Tensor]] = None, ptb0s: Optional[Sequence[torch.Tensor]] = None,
-                precision: str = "fp32", max_batch: int = 256) -> List[torch.Tensor]:
+                precision: str = "fp32", max_batch: int = 256, ragged: bool = False) -> List[torch.Tensor]:
     """emb / e2e / fb attack (attack_utils.py:51-86 / 7-48 / 89-130) of a list of utterances of any
     lengths: vc_tgts[i] [80, T_i], adv_tgts[i] [80, T'_i], vc_srcs[i] [80, S_i] (e2e / fb).
     Returns [vc_tgts[i] + eps * tanh(ptb_i)] ([80, T_i] each, on the first model's device).
@@ -95,10 +104,16 @@ def attack_many(kind: str, model_per_device: Sequence[torch.nn.Module], vc_tgts:
         if ptb0s[i].shape != vc_tgts[i].shape:
             raise ValueError(f"utterance {i}: ptb0 {tuple(ptb0s[i].shape)} != vc_tgt {tuple(vc_tgts[i].shape)}")
 
-    # the attack chunks: equal (T, S) within a chunk
+    if ragged and kind != "emb":
+        raise ValueError("ragged batches are built for the emb attack only")
+    # the attack chunks: equal (T, S) within a chunk -- or, ragged, any lengths, longest first
     keys = [(vc_tgts[i].shape[1], vc_srcs[i].shape[1] if vc_srcs is not None else 0) for i in range(n)]
-    chunks = buckets(keys, max_batch)
-    owner = assign([len(c) * keys[c[0]][0] * max(n_iters, 1) for c in chunks], len(devs))
+    if ragged:
+        order = sorted(range(n), key=lambda i: (-keys[i][0], i))
+        chunks = [order[s:s + max_batch] for s in range(0, n, max_batch)]
+    else:
+        chunks = buckets(keys, max_batch)
+    owner = assign([sum(keys[i][0] for i in c) * max(n_iters, 1) for c in chunks], len(devs))
     # per device: the adv_tgt embeddings it needs, grouped by adv_tgt length
     need = [sorted({i for j in owner[d] for i in chunks[j]}) for d in range(len(devs))]
     results: List[Optional[torch.Tensor]] = [None] * n
@@ -116,7 +131,7 @@ def attack_many(kind: str, model_per_device: Sequence[torch.nn.Module], vc_tgts:
                 # distinct shapes this device runs: embeddings, attacks (+ their forward plans);
                 # the cache holds them all, so a repeated call over the same lengths re-plans nothing
                 shapes = {(len(g), adv_tgts[need[d][g[0]]].shape[1]) for g in adv_groups}
-                shapes |= {(len(chunks[j]), keys[chunks[j][0]][0]) for j in owner[d]}
+                shapes |= {(len(chunks[j]), keys[chunks[j][0]][0]) if not ragged else tuple(chunks[j]) for j in owner[d]}
                 # e2e / fb: the ContentEncoder / Decoder workspaces are keyed by (B, T, T_src) and share
                 # the cap with the SpeakerEncoder ones
                 vc_shapes = {(len(chunks[j]),) + tuple(keys[chunks[j][0]]) for j in owner[d]} if kind != "emb" else set()
@@ -130,6 +145,14 @@ def attack_many(kind: str, model_per_device: Sequence[torch.nn.Module], vc_tgts:
                         emb[i] = e[k]
                 for j in owner[d]:
                     ids = chunks[j]
+                    if ragged:
+                        te = torch.stack([emb[i] for i in ids]).contiguous()
+                        outs, _, _ = ctx.emb_attack_ragged([vc_tgts[i].to(dev, torch.float32) for i in ids], te,
+                                                           [ptb0s[i].to(dev, torch.float32) for i in ids], eps, n_iters,
+                                                           precision=precision)
+                        for k, i in enumerate(ids):
+                            results[i] = outs[k]
+                        continue
                     vc = torch.stack([vc_tgts[i] for i in ids]).to(dev, torch.float32).contiguous()
                     p0 = torch.stack([ptb0s[i] for i in ids]).to(dev, torch.float32).contiguous()
                     te = torch.stack([emb[i] for i in ids]).contiguous()

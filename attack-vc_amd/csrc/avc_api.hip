@@ -179,6 +179,13 @@ struct Workspace {
     DevBuf hdr, hdr_m, hdr_v, hdr_gx; // header [F*T], its Adam state, d loss / d x [N][F*T]
     bool built = false;
     int gen = 0;                      // ctx-unique id of this workspace's current plans (set on every (re)plan)
+    // ragged batch (avc_emb_attack_ragged): utterance b has lens[b] frames; inputs / Adam state are packed
+    // [80][lens[b]] blocks; long engine, scratch sized for T = the longest
+    bool ragged = false;
+    std::vector<int> lens;
+    RagUtt* rag = nullptr;            // device [B]: lengths, per-block lengths, packed offsets
+    double flop_fwd = 0;              // algorithmic FLOPs of one SpeakerEncoder pass over the batch
+    size_t X = 0;                     // floats of one input / state array (B x 80 x T, or the packed sum)
 };
 
 }  // namespace
@@ -762,6 +769,10 @@ static void free_ws(Workspace& ws) {
     if (ws.lza.fl[0]) hipFree(ws.lza.fl[0]);
     if (ws.lza.masks) hipFree(ws.lza.masks);
     ws.lza = LongArgs{};
+    if (ws.rag) hipFree(ws.rag);
+    ws.rag = nullptr;
+    ws.ragged = false;
+    ws.lens.clear();
     ws.fused = false;
     ws.lz = false;
     ws.built = false;
@@ -1163,6 +1174,7 @@ static FusedArgs fused_args(avc_ctx* ctx, Workspace& ws, int prec) {
     A.scal = ws.scal.p;
     A.table_len = ws.iters_cap;
     A.w = ctx->fzw[prec];
+    A.rag = ws.rag;
     return A;
 }
 
@@ -1194,7 +1206,7 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
     F.fz.write_masks = attack ? 1 : 0;
     F.fz.tick = attack ? ws.step : nullptr;
     F.fz_shape = fused_shape(ctx, ws.T);
-    F.flop = fz_fwd_flop(c, ws.Tl, ctx->bank_k) * B;
+    F.flop = ws.flop_fwd;
     F.name = prec == PREC_F32 ? "se_fwd_fused<f32>" : "se_fwd_fused<bf16>";
     if (ws.lz) F.name = prec == PREC_F32 ? "lz_se_fwd<f32>" : "lz_se_fwd<bf16>";
 
@@ -1277,7 +1289,7 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
     A.b2 = 0.999f;
     A.b2c = (float)(1.0 - 0.999);
     A.adam_eps = 1e-8f;
-    L.flop = fz_fwd_flop(ctx->cfg, ws.Tl, ctx->bank_k) * ws.B;   // input-gradient only
+    L.flop = ws.flop_fwd;   // input-gradient only
     L.name = prec == PREC_F32 ? "se_bwd_fused<f32>" : "se_bwd_fused<bf16>";
     if (ws.lz) L.name = prec == PREC_F32 ? "lz_se_bwd<f32>" : "lz_se_bwd<bf16>";
     pl.launches.push_back(L);
@@ -1373,11 +1385,10 @@ static int drop_ws(avc_ctx* ctx) {
     return 1;
 }
 
-static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
+// lengths through the conv blocks for T input frames + reflect-pad validity (torch: pad < input length)
+static int enc_block_lengths(avc_ctx* ctx, int T, std::vector<int>& Tl) {
     const avc_se_cfg& c = ctx->cfg;
-    if (B <= 0) return fail("batch size must be positive (got %d)", B);
-    // lengths through the blocks + reflect-pad validity (torch: pad < input length)
-    std::vector<int> Tl{T};
+    Tl.assign(1, T);
     int maxpad = 0;
     for (int k : ctx->bank_k) {
         int a, b;
@@ -1397,16 +1408,48 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         if (To != Tp) return fail("conv/pool length mismatch at block %d (%d vs %d)", l, To, Tp);
         Tl.push_back(To);
     }
-    const int eng = engine_for(ctx, T);
+    return 0;
+}
+
+// The workspace of a call: B utterances of T frames, or (lens non-null) a ragged batch of B utterances
+// of lens[b] frames (long engine; T is ignored).  Cached by shape, most recently used first.
+static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters, const std::vector<int>* lens = nullptr) {
+    const avc_se_cfg& c = ctx->cfg;
+    if (B <= 0) return fail("batch size must be positive (got %d)", B);
+    std::vector<int> Tl;
+    std::vector<std::vector<int>> Tls;
+    double flop = 0;
+    size_t X = 0;
+    if (lens) {
+        if ((int)lens->size() != B) return fail("ragged batch: %zu lengths for B=%d", lens->size(), B);
+        if (!ctx->fused_ok || ctx->engine == AVC_ENGINE_LAYERED)
+            return fail("ragged batches run on the long engine (fused-capable config, engine not layered)");
+        T = *std::max_element(lens->begin(), lens->end());
+        for (int b = 0; b < B; ++b) {
+            std::vector<int> t;
+            if (enc_block_lengths(ctx, (*lens)[b], t)) return 1;
+            flop += fz_fwd_flop(c, t, ctx->bank_k);
+            X += (size_t)c.c_in * (*lens)[b];
+            Tls.push_back(t);
+        }
+    }
+    if (enc_block_lengths(ctx, T, Tl)) return 1;
+    if (!lens) {
+        flop = fz_fwd_flop(c, Tl, ctx->bank_k) * B;
+        X = (size_t)B * c.c_in * T;
+    }
+    const int eng = lens ? AVC_ENGINE_LONG : engine_for(ctx, T);
     const bool fused = eng != AVC_ENGINE_LAYERED, lz = eng == AVC_ENGINE_LONG;
     // a cached workspace of this shape (most recently used first)
     auto it = ctx->wss.begin();
     for (; it != ctx->wss.end(); ++it)
-        if (it->built && it->B == B && it->T == T && it->fused == fused && it->lz == lz) break;
+        if (it->built && it->ragged == (lens != nullptr) &&
+            (lens ? it->lens == *lens : (it->B == B && it->T == T && it->fused == fused && it->lz == lz)))
+            break;
     static const bool dbg_ws = getenv("AVC_DEBUG_WS") && getenv("AVC_DEBUG_WS")[0] == '1';
     if (dbg_ws)
-        fprintf(stderr, "AVC_DEBUG_WS ensure_ws B=%d T=%d fused=%d lz=%d n=%d: %s (%zu cached)\n", B, T, (int)fused,
-                (int)lz, n_iters, it != ctx->wss.end() ? "hit" : "new", ctx->wss.size());
+        fprintf(stderr, "AVC_DEBUG_WS ensure_ws B=%d T=%d fused=%d lz=%d ragged=%d n=%d: %s (%zu cached)\n", B, T,
+                (int)fused, (int)lz, (int)(lens != nullptr), n_iters, it != ctx->wss.end() ? "hit" : "new", ctx->wss.size());
     if (it != ctx->wss.end()) {
         ctx->wss.splice(ctx->wss.begin(), ctx->wss, it);
         ctx->cur = &ctx->wss.front();
@@ -1437,10 +1480,25 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters) {
         ws.B = B;
         ws.T = T;
         ws.Tl = Tl;
+        ws.X = X;
+        ws.flop_fwd = flop;
         const int nb = ctx->nb;
-        const size_t X = (size_t)B * c.c_in * T;
         ws.fused = fused;
         ws.lz = lz;
+        if (lens) {
+            ws.ragged = true;
+            ws.lens = *lens;
+            std::vector<RagUtt> ru(B);
+            int64_t off = 0;
+            for (int b = 0; b < B; ++b) {
+                ru[b] = RagUtt{};
+                ru[b].T = (*lens)[b];
+                ru[b].xoff = off;
+                off += (int64_t)c.c_in * (*lens)[b];
+            }
+            WSCHK(hipMalloc(&ws.rag, B * sizeof(RagUtt)));
+            WSCHK(hipMemcpy(ws.rag, ru.data(), B * sizeof(RagUtt), hipMemcpyHostToDevice));
+        }
         int rc = 0;
         for (DevBuf* b : {&ws.xin, &ws.adv, &ws.vc, &ws.ptb, &ws.m, &ws.v, &ws.grad0}) rc |= dalloc(*b, X);
         for (DevBuf* b : {&ws.emb_fwd, &ws.org, &ws.tgt}) rc |= dalloc(*b, (size_t)B * c.c_out);
@@ -1938,7 +1996,7 @@ static int graph_replay(avc_ctx* ctx, Plan& iter, hipGraphExec_t& graph, int n_i
 // tgt_emb [B][c_out] (adv_tgt of another length, embedded beforehand by avc_se_forward)
 static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_tgt, const float* tgt_emb,
                            const float* ptb0, int B, int T, float eps, int n_iters, float* out_adv,
-                           const avc_attack_opts* opts, void* stream) {
+                           const avc_attack_opts* opts, void* stream, const std::vector<int>* lens = nullptr) {
     if (!ctx || !vc_tgt || !(adv_tgt || tgt_emb) || !ptb0 || !out_adv) return fail("avc_emb_attack: null argument");
     if (n_iters < 0) return fail("n_iters must be >= 0");
     avc_attack_opts o{};
@@ -1950,7 +2008,7 @@ static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_t
     if (o.update != AVC_UPDATE_ADAM && !(o.update == AVC_UPDATE_PGD && o.pgd_step > 0.f))
         return fail("bad update %d (PGD needs pgd_step > 0)", o.update);
     hipStream_t us = (hipStream_t)stream;
-    if (ensure_ws(ctx, B, T, n_iters)) return 1;
+    if (ensure_ws(ctx, B, T, n_iters, lens)) return 1;
     Workspace& ws = *ctx->cur;
     const bool bf16 = o.precision == AVC_PREC_BF16;
     if (bf16 && ws.iter_bf16.launches.empty()) {
@@ -1967,7 +2025,7 @@ static int emb_attack_impl(avc_ctx* ctx, const float* vc_tgt, const float* adv_t
     hipGraphExec_t& graph = bf16 ? ws.graph_bf16 : ws.graph;
     if (begin_call(ctx, us)) return 1;
     const avc_se_cfg& c = ctx->cfg;
-    const size_t X = (size_t)B * c.c_in * T;
+    const size_t X = ws.X;   // B x 80 x T, or a ragged batch's packed sum
     const float gscale = (float)(2.0 / (o.reduction == AVC_REDUCE_MEAN ? (double)B * c.c_out : (double)c.c_out));
 
     const float scal[4] = {eps, gscale, 0.f, o.update == AVC_UPDATE_PGD ? o.pgd_step : 0.f};
@@ -2032,6 +2090,20 @@ extern "C" int avc_emb_attack_emb(avc_ctx* ctx, const float* vc_tgt, const float
                                   void* stream) {
     if (!tgt_emb) return fail("avc_emb_attack_emb: null argument");
     return emb_attack_impl(ctx, vc_tgt, nullptr, tgt_emb, ptb0, B, T, eps, n_iters, out_adv, opts, stream);
+}
+
+// A ragged batch: utterance b has lengths[b] frames (host array); vc_tgt / ptb0 / out_adv (and opts->grad0)
+// are packed [80][lengths[b]] blocks in batch order, tgt_emb [B][c_out] = SE(adv_tgt_b) at adv_tgt_b's own
+// length.  One launch per pass over every length (the long engine with per-workgroup lengths).
+extern "C" int avc_emb_attack_ragged(avc_ctx* ctx, const float* vc_tgt, const int* lengths, int B, const float* tgt_emb,
+                                     const float* ptb0, float eps, int n_iters, float* out_adv,
+                                     const avc_attack_opts* opts, void* stream) {
+    if (!ctx || !lengths || !tgt_emb) return fail("avc_emb_attack_ragged: null argument");
+    if (B <= 0) return fail("avc_emb_attack_ragged: batch size must be positive (got %d)", B);
+    if (opts && opts->reduction != AVC_REDUCE_INDEPENDENT)
+        return fail("avc_emb_attack_ragged: only independent per-utterance attacks (reduction 0)");
+    const std::vector<int> lens(lengths, lengths + B);
+    return emb_attack_impl(ctx, vc_tgt, nullptr, tgt_emb, ptb0, B, 0, eps, n_iters, out_adv, opts, stream, &lens);
 }
 
 static int run_iterations(avc_ctx* ctx, Plan& iter, hipGraphExec_t& graph, int n_iters, bool use_graph);

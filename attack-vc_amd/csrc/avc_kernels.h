@@ -146,6 +146,16 @@ struct FusedW {
     const float* b_mean;
 };
 
+// Ragged batch (long engine, emb attack; avc_emb_attack_ragged): every workgroup's utterance has its own
+// length.  Its input / Adam state start at float offset xoff of the packed arrays ([80][T_b] blocks, one
+// after the other); the scratch slots (LongArgs) are sized for the longest.
+// (The block lengths follow from T: Tl[l+1] = ceil(Tl[l] / sub[l]), avc_long.hip lz_tl.)
+struct RagUtt {
+    int32_t T;
+    int32_t pad_;
+    int64_t xoff;
+};
+
 struct FusedArgs {
     int32_t B, T, nb, ks, nblk, act;
     int32_t sub[FZ_MAXBLK];
@@ -174,6 +184,8 @@ struct FusedArgs {
     float* loss_cur;                  // fwd writes / bwd reads: [B] this iteration's per-utterance loss
     float* losses;                    // bwd: [loss_len][B] loss history (row = step - 1), or null
     HeadArgs head;                    // fwd (fuse_head): weights, biases, targets, g_pooled out
+    const RagUtt* rag;                // long engine: per-workgroup lengths / offsets (null: every utterance
+                                      // T frames at b * 80 * T)
 };
 
 // ---------------------------------------------------------------------------------

@@ -486,6 +486,16 @@ __device__ __forceinline__ void lz_mom_get(LzMom& M, int Tl, f32x4 (&mean)[2], f
     M.n = 0.f;
 }
 
+// Input length of conv block l for T frames: ceil-mode pooling halves it at every stride-2 block
+// (models.py:303; the host's enc_block_lengths checks conv and pool agree).  Computed from the workgroup's
+// own T (a ragged batch has one per utterance) instead of indexing A.Tl: a select between a kernarg array
+// and a per-utterance global one made the compiler copy the whole FusedArgs to scratch (1.3 KB per lane).
+__device__ __forceinline__ int lz_tl(const FusedArgs& A, int T, int l) {
+    int t = T;
+    for (int k = 0; k < l; ++k) t = A.sub[k] == 2 ? (t + 1) >> 1 : t;
+    return t;
+}
+
 // ---------------------------------------------------------------------------------
 // forward: SpeakerEncoder (models.py:327-343) or, in ce_mode, ContentEncoder (181-210)
 // ---------------------------------------------------------------------------------
@@ -497,7 +507,10 @@ __device__ __forceinline__ void lz_se_fwd_body(FusedArgs A, LongArgs L) {
     constexpr int NF = LZ_CHF;
     constexpr bool DBUF = PREC == PREC_BF16;
     const int b = blockIdx.x;
-    const int T = A.T, nb = A.nb, nblk = A.nblk, ks = A.ks, P = ks / 2, act = A.act;
+    const RagUtt* const ru = A.rag ? A.rag + b : nullptr;   // ragged batch: this utterance's own length
+    const int T = ru ? ru->T : A.T, nb = A.nb, nblk = A.nblk, ks = A.ks, P = ks / 2, act = A.act;
+    auto Tl = [&](int l) __attribute__((always_inline)) { return lz_tl(A, T, l); };
+    const size_t xb = ru ? (size_t)ru->xoff : (size_t)b * FZ_CIN * T;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
@@ -552,7 +565,7 @@ __device__ __forceinline__ void lz_se_fwd_body(FusedArgs A, LongArgs L) {
         for (int k = 0; lz_chunk(k, nf0, NF, chk); ++k) {
             const int n0 = 16 * chk.f0;
             __syncthreads();                             // the previous chunk's readers are done
-            lz_x_window<PREC>(XB, A.x + (size_t)b * FZ_CIN * T, T, n0 - 4, NXR);
+            lz_x_window<PREC>(XB, A.x + xb, T, n0 - 4, NXR);
             __syncthreads();
             FZ_PH();
             f32x4 acc_h[2][NF];
@@ -670,7 +683,7 @@ __device__ __forceinline__ void lz_se_fwd_body(FusedArgs A, LongArgs L) {
     f32x4 tmean[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     char* WB = fz_lds;
     for (int l = 0; l < nblk; ++l) {
-        const int Ti = A.Tl[l], To = A.Tl[l + 1], s = A.sub[l];
+        const int Ti = Tl(l), To = Tl(l + 1), s = A.sub[l];
         const bool lastblk = l + 1 == nblk;
         f32x4 bc1[2], bc2[2];
 #pragma unroll
@@ -817,7 +830,7 @@ __device__ __forceinline__ void lz_se_fwd_body(FusedArgs A, LongArgs L) {
             });
         cur ^= 1;
     }
-    const int TN = A.Tl[nblk];
+    const int TN = Tl(nblk);
     if (ce) {
         // mean_layer (1x1, models.py:207): mu = W_mean h_N + b -> [128][TN]
         lz_publish();
@@ -890,7 +903,9 @@ __device__ __forceinline__ void lz_se_bwd_body(FusedArgs A, LongArgs L) {
     constexpr int VE = 16 / ESZ, KS = 4 * VE;
     constexpr int NF = LZ_CHF;
     const int b = blockIdx.x;
-    const int T = A.T, nb = A.nb, nblk = A.nblk, ks = A.ks, P = ks / 2, act = A.act;
+    const RagUtt* const ru = A.rag ? A.rag + b : nullptr;   // ragged batch: this utterance's own length
+    const int T = ru ? ru->T : A.T, nb = A.nb, nblk = A.nblk, ks = A.ks, P = ks / 2, act = A.act;
+    auto Tl = [&](int l) __attribute__((always_inline)) { return lz_tl(A, T, l); };
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
@@ -923,7 +938,7 @@ __device__ __forceinline__ void lz_se_bwd_body(FusedArgs A, LongArgs L) {
     ring_fill(ring, op_c2T(nblk - 1));
 
     // g(h_N) = d loss / d pooled / TN on every frame (AdaptiveAvgPool1d backward)
-    const int TN = A.Tl[nblk];
+    const int TN = Tl(nblk);
     f32x4 gN[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -933,7 +948,7 @@ __device__ __forceinline__ void lz_se_bwd_body(FusedArgs A, LongArgs L) {
     }
     // dY of the last block's conv2 = g(h_N) * act'(y2): dilated image rows LZ_ZR + s*t
     {
-        const int l = nblk - 1, To = A.Tl[l + 1], s = A.sub[l];
+        const int l = nblk - 1, To = Tl(l + 1), s = A.sub[l];
         for (int F = 0; F < lz_nf(To); ++F) {
             LzMask m;
             m.load(mbyte(nb + 2 + 2 * l, F));
@@ -955,7 +970,7 @@ __device__ __forceinline__ void lz_se_bwd_body(FusedArgs A, LongArgs L) {
     char* WB = fz_lds;
     int cur = 0;
     for (int l = nblk - 1; l >= 0; --l) {
-        const int Ti = A.Tl[l], To = A.Tl[l + 1], s = A.sub[l];
+        const int Ti = Tl(l), To = Tl(l + 1), s = A.sub[l];
         // zero rows around the dY2 image: before frame 0 and after frame s*To
         lz_zero_rows<PREC>(imgg, 0, LZ_ZR);
         lz_zero_rows<PREC>(imgg, LZ_ZR + s * To, LZ_ZR);
@@ -1130,7 +1145,7 @@ __device__ __forceinline__ void lz_se_bwd_body(FusedArgs A, LongArgs L) {
     const float bc2s = adam ? Ad.table[2 * (step - 1) + 1] : 1.f;
     const float rbc2s = 1.f / bc2s;
     const AdamStep S{nstep, bc2s, rbc2s, eps, adam ? A.scal[3] : 0.f};
-    const size_t xb = (size_t)b * FZ_CIN * T;
+    const size_t xb = ru ? (size_t)ru->xoff : (size_t)b * FZ_CIN * T;
     LzChunk chk;
     for (int k = 0; lz_chunk(k, nfx, CHF, chk); ++k) {
         const int n0 = 16 * chk.f0;

@@ -83,6 +83,11 @@ def parse():
                     help="CPU baseline (ii): concurrent 1-thread processes (the GPU box's CPU share is 16; "
                          "its process guard allows 16 processes with the GPU open, this one included)")
     ap.add_argument("--cpu-worker", type=float, default=0.0, help=argparse.SUPPRESS)
+    ap.add_argument("--lengths", default=None, metavar="MIN:MAX",
+                    help="emb attack over a seeded uniform mix of utterance lengths in [MIN, MAX] frames (real data: "
+                         "every utterance its own length), one ragged batch per GPU (attack_many(ragged=True))")
+    ap.add_argument("--bucketed", action="store_true",
+                    help="--lengths: per-length buckets (attack_many's default) instead of the ragged batch, for comparison")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: launcher + gloo rendezvous + sharding + timing, no attack computed")
     return ap.parse_args()
@@ -484,6 +489,151 @@ def main_mel2wav(a):
         dist.destroy_process_group()
 
 
+def cpu_baseline_lengths(sd, lens, budget_s, threads, mean_T):
+    """The reference loop (oracle/torch_cpu.py, B = 1) over utterances of the mix, for about budget_s
+    seconds: frame-iterations per second, scaled to utts/s of the mix (x 1500 iterations, mean length)."""
+    from oracle import torch_cpu
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(5)
+    done_fi, t_used, used = 0, 0.0, []
+    for T in lens:
+        vc, at, p0 = (torch.randn(1, 80, T, generator=g) for _ in range(3))
+        torch_cpu.emb_attack(sd, FULL_CFG, vc, at, 0.1, 1, p0)           # warm-up of this shape
+        stamps = []
+        t0 = time.perf_counter()
+
+        def hook(it):
+            stamps.append(time.perf_counter())
+            if stamps[-1] - t0 > budget_s / 4:
+                raise StopIteration
+        try:
+            torch_cpu.emb_attack(sd, FULL_CFG, vc, at, 0.1, 1500, p0, iter_hook=hook)
+        except StopIteration:
+            pass
+        done_fi += T * len(stamps)
+        t_used += stamps[-1] - t0
+        used.append(T)
+        if t_used > budget_s:
+            break
+    rate = done_fi / t_used                       # frame-iterations per second
+    return {"value": round(rate / (mean_T * 1500), 5), "unit": "utts/s", "cores": threads, "kind": "port",
+            "frames_per_s": round(rate / 1500, 2),
+            "sample": f"B=1 emb_attack of {len(used)} utterances of the mix ({used} frames), {done_fi} "
+                      f"frame-iterations in {t_used:.1f} s, scaled to the mix's mean length {mean_T:.1f} x 1500 "
+                      f"iterations; oracle/torch_cpu.py (reference ATen arithmetic)"}
+
+
+def main_lengths(a):
+    """Real-data lengths: B utterances per GPU, lengths uniform in [MIN, MAX] (seeded), adv_tgt of their own
+    seeded lengths; step = attack_many(ragged=True) -- the adv_tgt embeddings per length plus one ragged
+    1500-iteration attack over the rank's utterances (every pass one launch over all lengths)."""
+    lo, hi = (int(v) for v in a.lengths.split(":"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")   # host-side barrier / max only: no RCCL in the process
+    import avc_native
+    import batching
+    import models
+    import shard
+    torch.manual_seed(0)
+    model = models.AdaInVC(FULL_CFG)
+    model_dev = model.to(dev)
+    B = a.batch
+    total = B * world
+    g = torch.Generator().manual_seed(2)
+    lens_all = torch.randint(lo, hi + 1, (total,), generator=g).tolist()
+    alens_all = torch.randint(lo, hi + 1, (total,), generator=g).tolist()
+    sl = shard.shard_slice(total, rank, world)
+    lens, alens = lens_all[sl], alens_all[sl]
+    gi = torch.Generator().manual_seed(3 + rank)
+    vc = [torch.randn(80, t, generator=gi).to(dev) for t in lens]
+    at = [torch.randn(80, t, generator=gi).to(dev) for t in alens]
+    p0 = [torch.randn(80, t, generator=gi).to(dev) for t in lens]
+
+    def step(prec=a.precision, n=a.n_iters):
+        return batching.attack_many("emb", [model_dev], vc, at, a.eps, n, ptb0s=p0, precision=prec, max_batch=B,
+                                    ragged=not a.bucketed)
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, None)
+    assert all(torch.isfinite(o).all() for o in out)
+    frames = sum(lens_all)
+    roof = None
+    if not a.no_roofline:
+        ctx = avc_native.context_for(model_dev.speaker_encoder, dev)
+        te = torch.cat([ctx.se_forward(x[None]) for x in at])
+        order = sorted(range(len(lens)), key=lambda i: (-lens[i], i))   # attack_many's longest-first batch
+        vo, po = [vc[i] for i in order], [p0[i] for i in order]
+        ctx.ktime_start()
+        ctx.emb_attack_ragged(vo, te[order], po, a.eps, KTIME_ITERS, precision=a.precision)
+        kt = ctx.ktime_stop()
+        ctx.set_profiling(True)
+        ctx.emb_attack_ragged(vo, te[order], po, a.eps, PROF_ITERS, precision=a.precision)
+        ms_iter, stats = ctx.profile()
+        ctx.set_profiling(False)
+        peak, unit = PEAK[a.precision]
+        timed = {k: v for k, v in kt.items() if k in stats}
+        base, (kn, kus) = max(timed.items(), key=lambda kv: kv[1][0] * kv[1][1])
+        n, tot_ms, tot_fl = stats[base]
+        achieved = (tot_fl / n) / (kus * 1e-6) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 4), "traffic": None, "kernel": base, "avg_launch_ms": round(kus * 1e-3, 5),
+                "timing": f"in-graph device wall-clock stamps (avc_ktime), {kn} launches over {KTIME_ITERS} iterations",
+                "flop_per_launch": tot_fl / n,
+                "in_graph": {k: {"launches_per_iter": v[0] / KTIME_ITERS, "avg_ms": round(v[1] * 1e-3, 5)}
+                             for k, v in kt.items()},
+                "per_kernel": {k: {"launches_per_iter": v[0] / PROF_ITERS, "avg_ms": round(v[1] / v[0], 4)}
+                               for k, v in stats.items()}}
+        ppath = os.path.join(ROOT, "profiles", "pmc.json")
+        if os.path.exists(ppath):
+            rec = json.load(open(ppath)).get(f"emb_lengths_{lo}_{hi}", {}).get(base)
+            if rec is not None:
+                ver = avc_native.lib().avc_version().decode()
+                roof.update(traffic=rec["traffic"], mfma_util=rec["mfma_util"], pmc_source=rec["source"],
+                            pmc_src=rec.get("src"),
+                            pmc_stale=rec.get("src") is None or ("src=" + rec["src"]) not in ver)
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline_lengths({k: v.detach().cpu() for k, v in model.state_dict().items()}, lens[:8],
+                                   a.cpu_seconds, threads, frames / total)
+    if rank == 0:
+        value = total * a.steps / elapsed
+        print(json.dumps({
+            "metric": f"defended utts/sec @ n_iters={a.n_iters} eps={a.eps} emb-attack, utterance lengths uniform in "
+                      f"[{lo}, {hi}] frames; 1/2/4/8 MI355X", "value": round(value, 3), "unit": "utts/s",
+            "frames_per_s": round(frames * a.steps / elapsed, 1), "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
+            "config": {"workload": f"emb_attack of B={B}/GPU utterances, lengths uniform in [{lo}, {hi}] (seed 2; mean "
+                                   f"{frames / total:.1f} frames), adv_tgt of their own lengths, n_iters={a.n_iters}, "
+                                   f"eps={a.eps}; " + ("per-length buckets (batching.attack_many)" if a.bucketed else
+                                                       "one ragged batch per GPU (batching.attack_many(ragged=True))"),
+                       "batch_per_gpu": B, "lengths": [lo, hi], "mean_frames": round(frames / total, 2),
+                       "n_iters": a.n_iters, "eps": a.eps,
+                       "parallelism": f"dp{world} (independent utterance shards, no collective)"},
+            "roofline": roof, "cpu_baseline": cpu, "libavc": avc_native.lib().avc_version().decode()}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     if a.cpu_worker > 0:
@@ -496,6 +646,10 @@ def main():
         return main_pm(a)
     if a.attack == "mel2wav":
         return main_mel2wav(a)
+    if a.lengths:
+        if a.attack != "emb":
+            raise SystemExit("--lengths measures the emb attack")
+        return main_lengths(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

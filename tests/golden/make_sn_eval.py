@@ -10,7 +10,8 @@ buffers unchanged.  This fixture pins that path on full_sn_T128's model (seed 0)
   * inference(vc_src, vc_tgt) of the eval-mode model (u / v as initialised) and, to make the stored
     state non-trivial, inference again after one train-mode forward moved u / v;
   * the e2e attack at n = 10 per utterance in eval mode (the Decoder's weights then stay fixed):
-    adv and ptb0 (the reference function's own run);
+    adv and ptb0 (the reference function's own run), grad0 (make_golden.py's instrumented loop, bitwise
+    the same adv);
   * the u / v after all of it (must equal the ones before each eval-mode call).
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_sn_eval.py
@@ -24,7 +25,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-from make_golden import EPS, make_inputs, run_reference, sha  # noqa: E402
+from make_golden import EPS, instrumented, make_inputs, run_reference, sha  # noqa: E402
 from make_sn import SN_CFG, uv  # noqa: E402
 
 
@@ -59,17 +60,20 @@ def main(ref="/root/reference"):
     with torch.no_grad():
         out["inference_eval_uv1"] = m.inference(X["vc_src"], X["vc_tgt"]).numpy()
     seeds = [2000, 2001]
-    advs, ptb0s = [], []
+    advs, ptb0s, grads = [], [], []
     for b in range(2):
         args = [X[k][b:b + 1] for k in ("vc_src", "vc_tgt", "adv_tgt")]
         mr = copy.deepcopy(model).eval()
         advs.append(run_reference(au, "e2e", mr, *args, EPS, 10, seeds[b]))
-        torch.manual_seed(seeds[b])
-        ptb0s.append(torch.zeros_like(args[1]).normal_(0, 1))   # attack_utils.py:10, same seed
+        ins = instrumented("e2e", copy.deepcopy(model).eval(), *args, EPS, 10, seeds[b])
+        assert torch.equal(ins["adv"], advs[-1])                 # the same arithmetic, plus the gradient
+        ptb0s.append(ins["ptb0"])
+        grads.append(ins["grad0"])
         for k, v in uv(mr).items():
             assert np.array_equal(v, u0[k]), k
     out["e2e_adv_n10_eval"] = torch.cat(advs).detach().numpy()
     out["e2e_ptb0_eval"] = torch.cat(ptb0s).numpy()
+    out["e2e_grad0_eval"] = torch.cat(grads).numpy()
     path = os.path.join(HERE, "full_sn_eval_T128.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path))

@@ -14,8 +14,10 @@ backward's ReLU' words staged in LDS), which the fp32 tests do not 
 
 The e2e / fb cases take vc_src of another length than vc_tgt (T_src != T, as attack.py:49-56 loads them),
 so the bf16 Decoder kernels run at content lengths Tz = 15 / 13 / 8 (T_src = 120 / 100 / 64 -> the
-ContentEncoder's three stride-2 blocks); the iteration-0 loss (which is MSE of the bf16 Decoder's output)
-is checked against the fp32 one too (2 %).  A wrong index in the LDS-staged mask path of the bf16
+ContentEncoder's three stride-2 blocks); the iteration-0 loss (MSE of the bf16 Decoder's output against the
+fp32-precomputed targets) is checked against the fp32 one too, within 10 %: it is a small difference of
+nearby outputs (MSE(out, tgt) - 0.1 MSE(out, org), ~5e-4), so the outputs' bf16 rounding is amplified
+(measured 3.5 % at T = 120).  A wrong index in the LDS-staged mask path of the bf16
 generic backward would be deterministic and would pass every self-comparison (test_gpu_batching.py); the
 float64 oracle and the fp32 kernels catch it here."""
 import numpy as np
@@ -114,7 +116,7 @@ def test_vc_bf16_generic_lengths(full, kind, T, Ts, Ta):
     print(f"{kind} T={T} Ts={Ts} Ta={Ta}: grad0 cos bf16/fp32 {c32.min():.5f}, bf16/f64 {c64.min():.5f}; "
           f"loss0 rel {dl.max():.2e}; |adv16-adv32| n=100 {float((a16 - a32).abs().max()):.2e}")
     assert c32.min() >= 0.99 and c64.min() >= 0.99, (c32, c64)
-    assert dl.max() <= 2e-2, (l16, l32)
+    assert dl.max() <= 0.1, (l16, l32)
     assert float((a16 - a32).abs().max()) <= 2e-2
     a32 = FN[kind](m, *d[:3], 0.1, 1500, ptb0=d[3]).detach()
     a16 = FN[kind](m, *d[:3], 0.1, 1500, ptb0=d[3], precision="bf16").detach()

@@ -15,7 +15,9 @@ import pytest
 import torch
 
 import attack_utils
-from helpers import TOL_GRAD_REL_VC, check_adv, model_from_fixture, rel
+import models
+from helpers import TOL_ADV_MEAN_VC, TOL_GRAD_REL_VC, cfg_of, check_adv, model_from_fixture, rel
+from oracle import adain_vc as oracle
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -114,11 +116,31 @@ def test_sn_eval_mode(golden):
     out = m.inference(_dev(z["vc_src"]), _dev(z["vc_tgt"])).cpu().numpy()
     assert rel(out, z["inference_eval_uv1"]) <= 1e-4, rel(out, z["inference_eval_uv1"])
     m = copy.deepcopy(m0).to(DEV).eval()
-    adv = attack_utils.e2e_attack(m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
-                                  ptb0=_dev(z["e2e_ptb0_eval"]))
-    check_adv(adv.detach().cpu().numpy(), z["e2e_adv_n10_eval"], 10, kind="e2e")
+    adv, info = attack_utils.e2e_attack(m, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
+                                        ptb0=_dev(z["e2e_ptb0_eval"]), return_info=True)
+    g0, ref0 = info["grad0"].cpu().numpy(), z["e2e_grad0_eval"]
+    assert rel(g0, ref0) <= TOL_GRAD_REL_VC, rel(g0, ref0)
     for k, v in m.decoder.state_dict().items():
         assert torch.equal(v.cpu(), m0.decoder.state_dict()[k].cpu()), k
+    # The same attack with the eval-mode weights (weight_orig / u.(W v), oracle.spectral_norm_step) baked into a
+    # plain sn=False Decoder: isolates the eval-mode hook from the attack's own fp32 conditioning.  On this input
+    # the e2e objective takes an fp32 ReLU flip between iterations 5 and 10 (scripts/dbg/sn_eval_diag.py: GPU vs
+    # float64 5.7e-6 at n = 5, 7.3e-5 at n = 10 -- the baked plain Decoder equally, 7.25e-5), so adv at n = 10 is
+    # held to 2e-4 of the reference's run (mean within the VC bound) and to 1e-5 of the baked model.
+    wo = oracle.Weights({k: v.detach().cpu().numpy() for k, v in m0.state_dict().items()})
+    wo.sn_train = False
+    oracle.spectral_norm_step(wo)
+    cfg2 = cfg_of(z)
+    cfg2["Decoder"] = dict(cfg2["Decoder"], sn=False)
+    mb = models.AdaInVC(cfg2)
+    mb.load_state_dict({k: (torch.from_numpy(np.ascontiguousarray(wo.d[k])) if k.startswith("decoder.")
+                            else m0.state_dict()[k]) for k in mb.state_dict()})
+    mb = mb.to(DEV)
+    adv_b = attack_utils.e2e_attack(mb, _dev(z["vc_src"]), _dev(z["vc_tgt"]), _dev(z["adv_tgt"]), 0.1, 10,
+                                    ptb0=_dev(z["e2e_ptb0_eval"]))
+    assert float((adv - adv_b).abs().max()) <= 1e-5, float((adv - adv_b).abs().max())
+    d = np.abs(adv.detach().cpu().numpy().astype(np.float64) - z["e2e_adv_n10_eval"])
+    assert d.mean() <= TOL_ADV_MEAN_VC[10] and d.max() <= 2e-4, (d.mean(), d.max())
     # and back in train mode the hook iterates again (the buffers move)
     m.train()
     m.inference(_dev(z["vc_src"]), _dev(z["vc_tgt"]))
