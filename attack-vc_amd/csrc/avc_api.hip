@@ -143,7 +143,8 @@ struct Launch {
     HeadArgs head{};
     FusedArgs fz{};              // L_FZ_* / L_LZ_*: per-utterance SpeakerEncoder pass (prec = PREC_*)
     LongArgs lz{};               // L_LZ_*: the long engine's scratch
-    int fz_shape = 8;            // L_FZ_*: kernel shape SH (0 = standard config at T = 128, else 1|2|4|8)
+    int fz_shape = 8;            // L_FZ_*: kernel shape SH (0 = standard config at T = 128, 16 = standard config
+                                 // at 64 < T < 128 (runtime lengths), else 1|2|4|8)
     DecArgs dz{};                // L_DZ_*: per-utterance fused Decoder pass (shape: fz_shape 0 | 8)
     DenseArgs dn{};              // L_DENSE: batched conv_affine layer (or its transpose)
     HdrArgs hd{};                // L_HDR_*: the header optimiser's elementwise ends
@@ -488,7 +489,7 @@ static int set_fused_attrs() {
         {(const void*)se_bwd_fused<PREC_F32, SH>, fz_lds_bwd(PREC_F32, 128)},                \
         {(const void*)se_bwd_fused<PREC_BF16, SH>, fz_lds_bwd_launch(PREC_BF16, 128, SH, 25 * FZ_MASK_WORDS_PER_LAYER)}
     const std::pair<const void*, int> fns[] = {AVC_FZ_FNS(0), AVC_FZ_FNS(1), AVC_FZ_FNS(2), AVC_FZ_FNS(4),
-                                               AVC_FZ_FNS(8)};
+                                               AVC_FZ_FNS(8), AVC_FZ_FNS(16)};
 #undef AVC_FZ_FNS
     for (auto& fn : fns) HIPCHK(hipFuncSetAttribute(fn.first, hipFuncAttributeMaxDynamicSharedMemorySize, fn.second));
     for (const void* fn : {(const void*)lz_se_fwd<PREC_F32>, (const void*)lz_se_fwd<PREC_BF16>,
@@ -1187,6 +1188,12 @@ static int fused_shape(avc_ctx* ctx, int T) {
         if (c.subsample[l] != ((l & 1) ? 2 : 1)) std_cfg = false;
     const char* e = getenv("AVC_FUSED_STD");
     if (std_cfg && !(e && e[0] == '0')) return 0;
+    // the standard config at 64 < T < 128: the standard kernels' fragment classes with runtime lengths
+    bool std_rt = T > 64 && T < 128 && ctx->nb == 8 && c.kernel_size == 5 && c.n_conv_blocks == 6 && c.act == 0;
+    for (int l = 0; std_rt && l < 6; ++l)
+        if (c.subsample[l] != ((l & 1) ? 2 : 1)) std_rt = false;
+    const char* r = getenv("AVC_FUSED_RT");
+    if (std_rt && !(e && e[0] == '0') && !(r && r[0] == '0')) return 16;
     const int nf = cdiv(T, 16);
     return nf <= 1 ? 1 : nf <= 2 ? 2 : nf <= 4 ? 4 : 8;
 }
@@ -1250,7 +1257,7 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
     // fewer per iteration; AVC_FUSE_HEAD=0 keeps the separate se_head_v launch (A/B runs)
     const char* fe = getenv("AVC_FUSE_HEAD");
     // (standard shape only: the in-kernel chain is unrolled for its n_dense = 6)
-    if (attack && prec == PREC_BF16 && ctx->head_Wr16.p && c.c_h == FZ_C && c.c_out == FZ_C && !ws.lz && F.fz_shape == 0 &&
+    if (attack && prec == PREC_BF16 && ctx->head_Wr16.p && c.c_h == FZ_C && c.c_out == FZ_C && !ws.lz && (F.fz_shape == 0 || F.fz_shape == 16) &&
         c.n_dense_blocks == 6 && !(fe && fe[0] == '0')) {
         const size_t head_lds = (size_t)(4 * c.n_dense_blocks + 8) * FZ_C * sizeof(float);
         F.shmem = std::max(F.shmem, head_lds);
@@ -1633,6 +1640,7 @@ static hipError_t launch_one(const Launch& L, hipStream_t s, const KEv* ev = nul
                       : L.fz_shape == 1 ? AVC_FZ_K(1)
                       : L.fz_shape == 2 ? AVC_FZ_K(2)
                       : L.fz_shape == 4 ? AVC_FZ_K(4)
+                      : L.fz_shape == 16 ? AVC_FZ_K(16)
                                         : AVC_FZ_K(8);
 #undef AVC_FZ_K
         klaunch(ev, false, k, L.grid, L.block, L.shmem, s, L.fz);

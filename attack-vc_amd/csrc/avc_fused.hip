@@ -82,6 +82,11 @@ namespace avc {
 //                   layer's frame and fragment count is a compile-time constant;
 //   SH = 1,2,4,8  : any eligible config and T <= 16*SH; every layer runs SH fragments
 //                   (SH + 1 for dgrad outputs, which carry the pad-position columns).
+//   SH = 16       : the config.yaml model at any T in (64, 128] (round 6): the standard kernels'
+//                   compile-time fragment classes (8, 8, 4, 4, 2, 2, 1 -- upper bounds of every such
+//                   T's layer lengths) with the frame counts as runtime values; odd block lengths
+//                   take the ceil-mode pooling tail.  Real utterances of 65-127 frames then run at the
+//                   128-frame kernels' cost instead of the generic instances' ~2x.
 // Fragment counts are never runtime values: MFMA code under runtime per-fragment
 // guards produced wrong results on gfx950 for one-fragment layers.
 // ---------------------------------------------------------------------------------
@@ -90,8 +95,9 @@ namespace avc {
 // ---------------------------------------------------------------------------------
 template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
-    constexpr int STD = SH == 0 ? 1 : 0;
-    constexpr int G = SH == 0 ? 8 : SH;         // fragments per (non-dgrad) layer
+    constexpr int STD = (SH == 0 || SH == 16) ? 1 : 0;
+    constexpr bool RT = SH == 16;               // standard classes, runtime frame counts
+    constexpr int G = STD ? 8 : SH;             // fragments per (non-dgrad) layer
     using E = typename Fz<PREC>::E;
     constexpr int RS = Fz<PREC>::RS;
     constexpr int ESZ = (int)sizeof(E);
@@ -101,7 +107,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     // bf16, standard shape (ReLU, no ContentEncoder InstanceNorm there): bank / conv1 epilogues pack first
     constexpr bool PKRELU = AVC_FZ_PKRELU && PREC == PREC_BF16 && STD != 0;
     const int b = blockIdx.x;
-    const int T = STD ? StdSE::T : A.T;
+    const int T = (STD && !RT) ? StdSE::T : A.T;
     const int nb = STD ? StdSE::NB : A.nb;
     const int nblk = STD ? StdSE::NBLK : A.nblk;
     const int ks = STD ? StdSE::KSZ : A.ks;
@@ -344,7 +350,7 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
         fz_gemm<PREC, 2, NF, FZ_C, 1>(acc, nfo, ring, op_c2(l),
                                       l + 1 < nblk ? op_c1(l + 1) : (ce ? op_mean() : op_c2(l)), YB, rb);
         FZ_PH();
-        if (AVC_FZ_POOLDPP && STD != 0 && s == 2) {
+        if (AVC_FZ_POOLDPP && STD != 0 && s == 2 && (!RT || (Ti & 1) == 0)) {
             // the standard shape's stride-2 layers have even input lengths: every pooled frame averages a
             // pair.  The pair sum h[2t'] + h[2t'+1] is formed in place by a quad-permute DPP add (lane 2k
             // holds it; the same bits as the add below, fp addition being commutative), then one lane
@@ -427,10 +433,10 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     if constexpr (STD != 0) {
         static_for<0, StdSE::NBLK>([&](auto L) __attribute__((always_inline)) {
             constexpr int l = decltype(L)::value;
-            block(IC<StdSE::nf(StdSE::Tl(l))>{}, IC<StdSE::nf(StdSE::Tl(l + 1))>{}, l, StdSE::Tl(l),
-                  StdSE::Tl(l + 1), StdSE::sub(l));
+            block(IC<StdSE::nf(StdSE::Tl(l))>{}, IC<StdSE::nf(StdSE::Tl(l + 1))>{}, l, RT ? A.Tl[l] : StdSE::Tl(l),
+                  RT ? A.Tl[l + 1] : StdSE::Tl(l + 1), StdSE::sub(l));
         });
-        TN = StdSE::Tl(StdSE::NBLK);
+        TN = RT ? A.Tl[StdSE::NBLK] : StdSE::Tl(StdSE::NBLK);
     } else if (fz_std_sub(A)) {
         // the standard subsample pattern at another length: each block on the fragment count of its
         // own frames (G >> stride-2 blocks before it, at least 1) instead of the input's G -- the deeper
@@ -507,8 +513,9 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 // ---------------------------------------------------------------------------------
 template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
-    constexpr int STD = SH == 0 ? 1 : 0;
-    constexpr int G = SH == 0 ? 8 : SH;
+    constexpr int STD = (SH == 0 || SH == 16) ? 1 : 0;
+    constexpr bool RT = SH == 16;               // standard classes, runtime frame counts
+    constexpr int G = STD ? 8 : SH;
     using E = typename Fz<PREC>::E;
     constexpr int RS = Fz<PREC>::RS;
     constexpr int ESZ = (int)sizeof(E);
@@ -519,7 +526,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     constexpr int EB = 4;          // bank dgrad edge columns per side
     constexpr int WPL = FZ_MASK_WORDS_PER_LAYER / 4;
     const int b = blockIdx.x;
-    const int T = STD ? StdSE::T : A.T;
+    const int T = (STD && !RT) ? StdSE::T : A.T;
     const int nb = STD ? StdSE::NB : A.nb;
     const int ks = STD ? StdSE::KSZ : A.ks;
     const int P = ks / 2;
@@ -546,7 +553,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
 
     // g_pooled, then the first GEMM's weight ring and mask words, are issued before the
     // LDS clearing so their latency hides under it
-    const int TN = STD ? StdSE::Tl(StdSE::NBLK) : A.Tl[A.nblk];
+    const int TN = (STD && !RT) ? StdSE::Tl(StdSE::NBLK) : A.Tl[A.nblk];
     f32x4 gp[2];
     if constexpr (PREC == PREC_BF16 && STD != 0) {
         if (A.fuse_head == 3) {   // e2e / fb: the head's backward (se_head_v mode 3) runs here
@@ -712,8 +719,9 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     if constexpr (STD != 0) {
         static_for<0, StdSE::NBLK>([&](auto L) __attribute__((always_inline)) {
             constexpr int l = StdSE::NBLK - 1 - decltype(L)::value;
-            constexpr int Ti = StdSE::Tl(l), To = StdSE::Tl(l + 1);
-            block(IC<StdSE::nf(To)>{}, IC<StdSE::nf(Ti + 2 * (StdSE::KSZ / 2))>{}, l, Ti, To, StdSE::sub(l));
+            constexpr int Tic = StdSE::Tl(l), Toc = StdSE::Tl(l + 1);   // the classes' bounds
+            block(IC<StdSE::nf(Toc)>{}, IC<StdSE::nf(Tic + 2 * (StdSE::KSZ / 2))>{}, l, RT ? A.Tl[l] : Tic,
+                  RT ? A.Tl[l + 1] : Toc, StdSE::sub(l));
         });
     } else if (fz_std_sub(A)) {   // per-block fragment counts, as in the forward
         static_for<0, 6>([&](auto L) __attribute__((always_inline)) {
@@ -843,8 +851,9 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     // deterministic cross-wave sum: ((p0 + p2) + (p1 + p3)), then tanh' + Adam
     // rows padded by 4 floats at T = 128: the 4 lane groups (kq) of a store then start 16
     // banks apart instead of on the same 16 banks (a 4-way conflict)
-    const int TP = STD ? T + 4 : T;
-    auto rq = [&](int q) __attribute__((always_inline)) { return STD ? q + q / (StdSE::T / 4) : q; };
+    constexpr bool PADR = SH == 0;             // (runtime T: unpadded rows, no runtime division per access)
+    const int TP = PADR ? T + 4 : T;
+    auto rq = [&](int q) __attribute__((always_inline)) { return PADR ? q + q / (StdSE::T / 4) : q; };
     float* R0 = reinterpret_cast<float*>(fz_lds);
     float* R1 = R0 + FZ_CIN * TP;
     for (int phase = 0; phase < 2; ++phase) {
@@ -952,11 +961,13 @@ AVC_FZ_INST(PREC_F32, 1)
 AVC_FZ_INST(PREC_F32, 2)
 AVC_FZ_INST(PREC_F32, 4)
 AVC_FZ_INST(PREC_F32, 8)
+AVC_FZ_INST(PREC_F32, 16)
 AVC_FZ_INST(PREC_BF16, 0)
 AVC_FZ_INST(PREC_BF16, 1)
 AVC_FZ_INST(PREC_BF16, 2)
 AVC_FZ_INST(PREC_BF16, 4)
 AVC_FZ_INST(PREC_BF16, 8)
+AVC_FZ_INST(PREC_BF16, 16)
 #undef AVC_FZ_INST
 
 }  // namespace avc

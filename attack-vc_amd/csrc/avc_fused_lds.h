@@ -21,7 +21,7 @@ __host__ __device__ constexpr int fz_lds_bwd(int prec, int T) { return fz_lds_bw
 // launch size: the shape-generic bf16 backward (shape != 0) also holds the utterance's ReLU' words
 // (mask_words u64) after that (avc_fused.hip: MLDS) -- at most 94.7 + 57.6 KB at T = 128
 __host__ __device__ constexpr int fz_lds_bwd_launch(int prec, int T, int shape, int mask_words) {
-    return fz_lds_bwd(prec, T) + (shape != 0 && prec == PREC_BF16 ? 8 * mask_words : 0);
+    return fz_lds_bwd(prec, T) + (shape != 0 && shape != 16 && prec == PREC_BF16 ? 8 * mask_words : 0);
 }
 
 // fused Decoder (avc_vc.hip) at output length Tn: forward = block-input image + conv1

@@ -25,11 +25,15 @@
 //
 // Per-layer frame counts are runtime values, but every GEMM runs a compile-time number of
 // fragments (8 per chunk; columns past the layer are clamped reads and dropped writes).
+#ifndef LZ_ABL
+#define LZ_ABL 0             // timing ablations only (wrong results): 1 = no bank-forward mask stores
+#endif
 #ifndef LZ_RD
 #define LZ_RD 4              // weight-ring depth of the block / bank-forward GEMMs
 #endif
-#ifndef LZ_PIN
-#define AVC_FZ_RING_FREE 1   // no per-step scheduling barrier in the ring (fz_gemm_impl)
+#ifdef LZ_RING_FREE
+#define AVC_FZ_RING_FREE 1   // no per-step scheduling barrier in the ring (fz_gemm_impl).  Round 6 A/B at T = 400:
+                             // the pinned ring (default) is 1.6 % faster per emb iteration (1.1047 -> 1.0870 ms)
 #endif
 #include "avc_fused_core.h"
 #include "avc_ktime.h"
@@ -590,7 +594,8 @@ __device__ __forceinline__ void lz_se_fwd_body(FusedArgs A, LongArgs L) {
                     for (int i = 0; i < 2; ++i)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) y[i][r] = act_f(acc[i][f][r] + bkb[i][r], act);
-                    if (wm && chk.f0 + f < nf0 && chk.owns(16 * (chk.f0 + f))) *mbyte(kb, chk.f0 + f) = (unsigned char)lz_mask_bits(y);
+                    if (!(LZ_ABL & 1) && wm && chk.f0 + f < nf0 && chk.owns(16 * (chk.f0 + f)))
+                        *mbyte(kb, chk.f0 + f) = (unsigned char)lz_mask_bits(y);
 #pragma unroll
                     for (int i = 0; i < 2; ++i) st4<PREC>(BK + (16 * f + c) * RS + (ch0 + 16 * i) * ESZ, y[i]);
                 }
@@ -1245,44 +1250,78 @@ __device__ __forceinline__ void lz_se_bwd_body(FusedArgs A, LongArgs L) {
             __syncthreads();
         }
         FZ_PH();
-        // owned interior columns: t = n - 4 in [0, T).  UB elements per thread per batch, all
-        // their state loads issued before any arithmetic (one memory round trip per batch; 20:
-        // two round trips per 128-column chunk instead of ten)
-        constexpr int UB = 20;
-        for (int i0 = 0; i0 < FZ_CIN * CH; i0 += 256 * UB) {
-            size_t qv[UB];
-            bool ok[UB];
-            float gs[UB], P[UB], M[UB], V[UB], X[UB];
+        // owned interior columns: t = n - 4 in [0, T), in groups of 4 consecutive frames of one mel row.  The
+        // frame start n0 - 4 and the chunk's owned range are multiples of 4 (16), the utterance's offset xb a
+        // multiple of 80: with T a multiple of 4 (vec) a group is entirely owned and inside [0, T) or not at
+        // all, and every access is one 16-byte load / store; otherwise four 4-byte ones, each frame checked.
+        // UB4 groups per thread per round, their state loads issued before any arithmetic (one round trip
+        // per round; more groups per round spilled: the next chunk's ring5 prefetch is live here).  Same
+        // per-element arithmetic (adam_elem) either way.  (Round 6: the former per-element 4-byte loop took
+        // 31-56k cycles per 128-frame chunk at T = 400, 1.5-2x the fused engine's whole tail.)
+        const bool vec = (T & 3) == 0;
+        constexpr int NG = FZ_CIN * CH / 4, GPR = CH / 4, UG = (NG + 255) / 256, UB4 = 3;
+        auto ld4 = [&](const float* a, size_t q) __attribute__((always_inline)) {
+            if (vec) return ((const gf32x4*)(a))[q >> 2];
+            const __attribute__((address_space(1))) float* g = (const __attribute__((address_space(1))) float*)(a);
+            f32x4 r;
 #pragma unroll
-            for (int u = 0; u < UB; ++u) {
-                const int idx = i0 + tid + 256 * u;
-                const int ci = idx / CH, col = idx - ci * CH;
+            for (int e = 0; e < 4; ++e) r[e] = g[min(q + e, xb + (size_t)FZ_CIN * T - 1)];
+            return r;
+        };
+        auto st4g = [&](float* a, size_t q, f32x4 v, int nok) __attribute__((always_inline)) {
+            if (vec) {
+                ((gf32x4*)(a))[q >> 2] = v;
+                return;
+            }
+            __attribute__((address_space(1))) float* g = (__attribute__((address_space(1))) float*)(a);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (e < nok) g[q + e] = v[e];
+        };
+#pragma unroll 1
+        for (int u0 = 0; u0 < UG; u0 += UB4) {
+            f32x4 gs4[UB4], P4[UB4], M4[UB4], V4[UB4], X4[UB4];
+            size_t q4[UB4];
+            int nok[UB4];      // frames of the group to update (0..4)
+#pragma unroll
+            for (int u = 0; u < UB4; ++u) {
+                const int gi = tid + 256 * (u0 + u);
+                const int ci = min(gi / GPR, FZ_CIN - 1), col = 4 * (gi - (gi / GPR) * GPR);
                 const int n = n0 + col, t = n - 4;
-                ok[u] = idx < FZ_CIN * CH && chk.owns(n) && t >= 0 && t < T;
-                qv[u] = xb + (size_t)min(ci, FZ_CIN - 1) * T + min(max(t, 0), T - 1);
-                gs[u] = idx < FZ_CIN * CH ? R0[ci * CH + rcol(ci, col)] + R1[ci * CH + rcol(ci, col)] : 0.f;
+                nok[u] = (gi < NG && chk.owns(n) && t >= 0 && t < T) ? min(4, T - t) : 0;
+                q4[u] = xb + (size_t)ci * T + (size_t)min(max(t, 0), T - (vec ? 4 : 1));
+                const int lo = ci * CH + rcol(ci, col);
+                gs4[u] = *reinterpret_cast<const f32x4*>(R0 + lo) + *reinterpret_cast<const f32x4*>(R1 + lo);
                 if (adam) {
-                    P[u] = Ad.ptb[qv[u]];
-                    M[u] = Ad.m[qv[u]];
-                    V[u] = Ad.v[qv[u]];
-                    X[u] = Ad.vc[qv[u]];
+                    P4[u] = ld4(Ad.ptb, q4[u]);
+                    M4[u] = ld4(Ad.m, q4[u]);
+                    V4[u] = ld4(Ad.v, q4[u]);
+                    X4[u] = ld4(Ad.vc, q4[u]);
                 }
             }
 #pragma unroll
-            for (int u = 0; u < UB; ++u) {
-                if (!ok[u]) continue;
-                const size_t q = qv[u];
+            for (int u = 0; u < UB4; ++u) {
+                if (nok[u] == 0) continue;
                 if (!adam) {
-                    A.gx_out[q] = gs[u];
+                    st4g(A.gx_out, q4[u], gs4[u], nok[u]);
                     continue;
                 }
-                float p = P[u], mm = M[u], vv = V[u], g, ad;
-                adam_elem<PREC>(Ad, S, gs[u], X[u], p, mm, vv, g, ad);
-                if (Ad.grad0 && step == 1) Ad.grad0[q] = g;
-                Ad.ptb[q] = p;
-                Ad.m[q] = mm;
-                Ad.v[q] = vv;
-                Ad.adv[q] = ad;
+                f32x4 p = P4[u], mm = M4[u], vv = V4[u], g, ad;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float pe = p[e], me = mm[e], ve = vv[e], ge, ae;
+                    adam_elem<PREC>(Ad, S, gs4[u][e], X4[u][e], pe, me, ve, ge, ae);
+                    p[e] = pe;
+                    mm[e] = me;
+                    vv[e] = ve;
+                    g[e] = ge;
+                    ad[e] = ae;
+                }
+                if (Ad.grad0 && step == 1) st4g(Ad.grad0, q4[u], g, nok[u]);
+                st4g(Ad.ptb, q4[u], p, nok[u]);
+                st4g(Ad.m, q4[u], mm, nok[u]);
+                st4g(Ad.v, q4[u], vv, nok[u]);
+                st4g(Ad.adv, q4[u], ad, nok[u]);
             }
         }
         FZ_PH();
