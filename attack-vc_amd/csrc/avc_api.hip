@@ -1187,6 +1187,8 @@ static int fused_shape(avc_ctx* ctx, int T) {
     for (int l = 0; std_cfg && l < 6; ++l)
         if (c.subsample[l] != ((l & 1) ? 2 : 1)) std_cfg = false;
     const char* e = getenv("AVC_FUSED_STD");
+    const char* rf = getenv("AVC_FUSED_RT_FORCE");   // A/B runs: the runtime-length kernels at T = 128 too
+    if (std_cfg && rf && rf[0] == '1') return 16;
     if (std_cfg && !(e && e[0] == '0')) return 0;
     // the standard config at 64 < T < 128: the standard kernels' fragment classes with runtime lengths
     bool std_rt = T > 64 && T < 128 && ctx->nb == 8 && c.kernel_size == 5 && c.n_conv_blocks == 6 && c.act == 0;
@@ -1283,7 +1285,8 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
     L.fz = fused_args(ctx, ws, prec);
     L.lz = ws.lza;
     L.fz_shape = fused_shape(ctx, ws.T);
-    L.shmem = ws.lz ? LZ_SHMEM : fz_lds_bwd_launch(prec, ws.T, L.fz_shape, L.fz.mask_words);
+    // (SH = 16: the LDS images are laid out for the 128-frame bound)
+    L.shmem = ws.lz ? LZ_SHMEM : fz_lds_bwd_launch(prec, L.fz_shape == 16 ? 128 : ws.T, L.fz_shape, L.fz.mask_words);
     AdamArgs& A = L.fz.adam;
     A.ptb = ws.ptb.p;
     A.m = ws.m.p;

@@ -515,6 +515,9 @@ template <int PREC, int SH>
 __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     constexpr int STD = (SH == 0 || SH == 16) ? 1 : 0;
     constexpr bool RT = SH == 16;               // standard classes, runtime frame counts
+    // the 128-frame LDS layout with unconditional stores (bf16; the fp32 instance of it crashes the gfx950
+    // backend's AGPR-copy rewrite, so fp32 keeps the guarded stores)
+    constexpr bool RTU = RT && PREC == PREC_BF16;
     constexpr int G = STD ? 8 : SH;
     using E = typename Fz<PREC>::E;
     constexpr int RS = Fz<PREC>::RS;
@@ -597,11 +600,17 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     MaskRd mnext;
     if constexpr (!MLDS) mnext.load(mwords(nb + 2 + 2 * (nblk - 1)));
 
-    char* GB = fz_lds;                          // dilated dY image [T+2ZP] rows
-    char* GB2 = GB + (T + 2 * ZP) * RS;         // stride-1 dY image [T+2ZP] rows
-    float* FSCR = reinterpret_cast<float*>(fz_lds + fz_lds_bwd_main(PREC, T)) + w * (5 * 16 * 8);
+    // Runtime lengths (RT): the LDS images are laid out for the classes' bound (128 frames), so every store of
+    // a fragment's frames can be unconditional -- a frame past a layer's end stores a zero, which is what
+    // the zero-padded dgrad images hold there.  (Per-lane `t < T` store guards under runtime lengths cost
+    // exec-mask branches whose joins the waitcnt pass answers with full drains: the 36 us the SH = 16
+    // backward took over SH = 0 at the same T = 128, round-6 ablation.)
+    const int TL = RTU ? StdSE::T : T;
+    char* GB = fz_lds;                          // dilated dY image [TL+2ZP] rows
+    char* GB2 = GB + (TL + 2 * ZP) * RS;        // stride-1 dY image [TL+2ZP] rows
+    float* FSCR = reinterpret_cast<float*>(fz_lds + fz_lds_bwd_main(PREC, TL)) + w * (5 * 16 * 8);
     {   // zero both images (pad rows and dilation holes must read as 0)
-        const int n16 = 2 * (T + 2 * ZP) * RS / 16;
+        const int n16 = 2 * (TL + 2 * ZP) * RS / 16;
         for (int i = tid; i < n16; i += 256) reinterpret_cast<f32x4*>(fz_lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
@@ -635,7 +644,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     for (int r = 0; r < 4; ++r)
                         v[r] = mnext.gate(i, f, r, gh[i][f][r], act);
                     const int t = 16 * f + c;
-                    if (t < To) {
+                    if (RTU || t < To) {   // RTU: g(h_{l+1}) is zero past To (the row gets its zero)
                         st4<PREC>(GB + (ZP + s * t) * RS + (ch0 + 16 * i) * ESZ, v);
                         if (s == 2)
                             st4<PREC>(GB + (ZP + 2 * t + 1) * RS + (ch0 + 16 * i) * ESZ, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -671,7 +680,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
                     for (int r = 0; r < 4; ++r)
                         v[r] = m1.gate(i, f, r, acc[i][f][r], act);
                     const int t = 16 * f + c;
-                    if (t < Ti) st4<PREC>(GB2 + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
+                    if constexpr (RTU) {
+                        st4<PREC>(GB2 + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, t < Ti ? v : f32x4{0.f, 0.f, 0.f, 0.f});
+                    } else {
+                        if (t < Ti) st4<PREC>(GB2 + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
+                    }
                 }
         }
         __syncthreads();
@@ -745,7 +758,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = mnext.gate(i, f, r, gh[i][f][r], act);
             const int t = 16 * f + c;
-            if (t < T) st4<PREC>(GP + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);
+            if (RTU || t < T) st4<PREC>(GP + (ZP + t) * RS + (ch0 + 16 * i) * ESZ, v);   // (RT: g(h0) zero past T)
         }
     __syncthreads();
     FZ_PH();
@@ -818,7 +831,11 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = mb.gate(i, f, r, acc[i][f][r], act);
                 const int t = 16 * f + c;
-                if (t < T) st4<PREC>(GBK + (ZPB + t) * RS + (ch0 + 16 * i) * ESZ, v);
+                if constexpr (RTU) {
+                    st4<PREC>(GBK + (ZPB + t) * RS + (ch0 + 16 * i) * ESZ, t < T ? v : f32x4{0.f, 0.f, 0.f, 0.f});
+                } else {
+                    if (t < T) st4<PREC>(GBK + (ZPB + t) * RS + (ch0 + 16 * i) * ESZ, v);
+                }
             }
         asm volatile("" ::: "memory");   // wave-local hand-off (see above): program order only
         if (kb + 1 < nb) {
@@ -851,9 +868,9 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     // deterministic cross-wave sum: ((p0 + p2) + (p1 + p3)), then tanh' + Adam
     // rows padded by 4 floats at T = 128: the 4 lane groups (kq) of a store then start 16
     // banks apart instead of on the same 16 banks (a 4-way conflict)
-    constexpr bool PADR = SH == 0;             // (runtime T: unpadded rows, no runtime division per access)
-    const int TP = PADR ? T + 4 : T;
-    auto rq = [&](int q) __attribute__((always_inline)) { return PADR ? q + q / (StdSE::T / 4) : q; };
+    // (RT: the same padded layout of the classes' bound -- 132-float rows -- every column stored)
+    const int TP = (STD && !RT) || RTU ? TL + 4 : T;
+    auto rq = [&](int q) __attribute__((always_inline)) { return (STD && !RT) ? q + q / (StdSE::T / 4) : q; };
     float* R0 = reinterpret_cast<float*>(fz_lds);
     float* R1 = R0 + FZ_CIN * TP;
     for (int phase = 0; phase < 2; ++phase) {
@@ -865,7 +882,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
 #pragma unroll
                 for (int f = 0; f < 8; ++f) {
                     const int t = 16 * f + c;
-                    if (t >= T) continue;
+                    if (!RTU && t >= T) continue;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         float* p = R + (16 * i + 4 * kq + r) * TP + t;
@@ -880,6 +897,45 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     if (A.gx_out && A.losses && tid == 0) {   // fb: the fused head's loss of SE(dec) -> history row
         const int sn = *A.step;
         if (sn >= 1 && sn <= A.loss_len) A.losses[(size_t)(sn - 1) * A.B + b] = A.loss_cur[b];
+    }
+    // RT: item k of a thread is (row ci, frames 4g .. 4g+3) of the padded [80][132] rows, g < 32; its frames
+    // t < T are element (ci, t) of the utterance's [80][T] arrays (16-byte accesses when T is a multiple of 4)
+    const bool vec4 = (T & 3) == 0;
+    const size_t xbase = (size_t)b * FZ_CIN * T;
+    auto rt_item = [&](int k, int& ci, int& g4, int& nok) __attribute__((always_inline)) {
+        const int it = tid + 256 * k;          // < 80 * 32 = 2560 = 10 * 256
+        ci = it >> 5;
+        g4 = 4 * (it & 31);
+        nok = max(0, min(4, T - g4));
+    };
+    auto rt_ld = [&](const float* a, size_t q) __attribute__((always_inline)) {
+        if (vec4) return *reinterpret_cast<const f32x4*>(a + q);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = a[min(q + e, xbase + (size_t)FZ_CIN * T - 1)];
+        return v;
+    };
+    auto rt_st = [&](float* a, size_t q, f32x4 v, int nok) __attribute__((always_inline)) {
+        if (vec4) {
+            *reinterpret_cast<f32x4*>(a + q) = v;
+            return;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (e < nok) a[q + e] = v[e];
+    };
+    if (RTU && A.gx_out) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            int ci, g4, nok;
+            rt_item(k, ci, g4, nok);
+            if (nok == 0) continue;
+            const int lo = ci * TP + g4;
+            rt_st(A.gx_out, xbase + (size_t)ci * T + g4,
+                  *reinterpret_cast<const f32x4*>(R0 + lo) + *reinterpret_cast<const f32x4*>(R1 + lo), nok);
+        }
+        ktime_end(kt, kts);
+        return;
     }
     if (A.gx_out) {   // d loss / d x handed on (fb: the decoder output's gradient)
         f32x4* gx = reinterpret_cast<f32x4*>(A.gx_out + (size_t)b * FZ_CIN * T);
@@ -913,6 +969,48 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     f32x4* __restrict__ g04 = Ad.grad0 && step == 1 ? reinterpret_cast<f32x4*>(Ad.grad0) + base4 : nullptr;
     const f32x4* R04 = reinterpret_cast<const f32x4*>(R0);
     const f32x4* R14 = reinterpret_cast<const f32x4*>(R1);
+    if constexpr (RTU) {   // the class-layout items (see rt_item): one batch, loads first
+        constexpr int AB = 10;
+        f32x4 sP[AB], sM[AB], sV[AB], sX[AB];
+        size_t qa[AB];
+        int nk[AB], lo[AB];
+#pragma unroll
+        for (int k = 0; k < AB; ++k) {
+            int ci, g4;
+            rt_item(k, ci, g4, nk[k]);
+            qa[k] = xbase + (size_t)ci * T + min(g4, T - (vec4 ? 4 : 1));
+            lo[k] = ci * TP + g4;
+            sP[k] = rt_ld(Ad.ptb, qa[k]);
+            sM[k] = rt_ld(Ad.m, qa[k]);
+            sV[k] = rt_ld(Ad.v, qa[k]);
+            sX[k] = rt_ld(Ad.vc, qa[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < AB; ++k) {
+            if (nk[k] == 0) continue;
+            const f32x4 gsum = *reinterpret_cast<const f32x4*>(R0 + lo[k]) + *reinterpret_cast<const f32x4*>(R1 + lo[k]);
+            f32x4 p = sP[k], mm = sM[k], vv = sV[k], g, ad;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float pe = p[e], me = mm[e], ve = vv[e], ge, ae;
+                adam_elem<PREC>(Ad, S, gsum[e], sX[k][e], pe, me, ve, ge, ae);
+                p[e] = pe;
+                mm[e] = me;
+                vv[e] = ve;
+                g[e] = ge;
+                ad[e] = ae;
+            }
+            if (Ad.grad0 && step == 1) rt_st(Ad.grad0, qa[k], g, nk[k]);
+            rt_st(Ad.ptb, qa[k], p, nk[k]);
+            rt_st(Ad.m, qa[k], mm, nk[k]);
+            rt_st(Ad.v, qa[k], vv, nk[k]);
+            rt_st(Ad.adv, qa[k], ad, nk[k]);
+        }
+        FZ_PH();
+        FZ_PH_DUMP("bwd");
+        ktime_end(kt, kts);
+        return;
+    }
     // one batch of 16-byte accesses covers the utterance (80 x T / 4 <= 256 * AB at T <= 128);
     // all its loads are issued before its arithmetic (one HBM round trip)
     const int n4 = FZ_CIN * T / 4;
