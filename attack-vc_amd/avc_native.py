@@ -574,7 +574,8 @@ class Context:
 
     # --- profiling (bench.py roofline) ---------------------------------------------
     KTIME_KERNELS = tuple(f"{k}<{p}>" for k in ("se_fwd_fused", "se_bwd_fused", "lz_se_fwd", "lz_se_bwd", "lz_dec_fwd",
-                                                 "lz_dec_bwd", "dec_fwd_fused", "dec_bwd_fused") for p in ("f32", "bf16"))
+                                                 "lz_dec_bwd", "dec_fwd_fused", "dec_bwd_fused", "se_attack_fused")
+                         for p in ("f32", "bf16"))
 
     def ktime_start(self):
         """Start in-graph kernel timing (avc_ktime): device wall-clock stamps in the hot kernels."""
@@ -583,8 +584,8 @@ class Context:
     def ktime_stop(self) -> Dict[str, Tuple[int, float]]:
         """Stop in-graph kernel timing: {kernel: (launches, average launch microseconds)} for the
         kernels that ran."""
-        us = (ctypes.c_double * 16)()
-        n = (ctypes.c_int64 * 16)()
+        us = (ctypes.c_double * 18)()
+        n = (ctypes.c_int64 * 18)()
         _check(lib().avc_ktime(self.h, 0, us, n))
         return {k: (int(n[i]), float(us[i])) for i, k in enumerate(self.KTIME_KERNELS) if n[i] > 0}
 

@@ -129,10 +129,11 @@ int main(int argc, char** argv) {
     // the recording run's launches end with a serialised atomic tail)
     const char* kte = getenv("AVC_BENCH_KTIME");
     if (!(kte && kte[0] == '0')) {
-        static const char* const kn[8] = {"se_fwd_fused", "se_bwd_fused", "lz_se_fwd",     "lz_se_bwd",
-                                          "lz_dec_fwd",   "lz_dec_bwd",   "dec_fwd_fused", "dec_bwd_fused"};
-        double us[16];
-        int64_t nl[16];
+        static const char* const kn[9] = {"se_fwd_fused", "se_bwd_fused",  "lz_se_fwd",
+                                          "lz_se_bwd",    "lz_dec_fwd",    "lz_dec_bwd",
+                                          "dec_fwd_fused", "dec_bwd_fused", "se_attack_fused"};
+        double us[18];
+        int64_t nl[18];
         CK(avc_ktime(ctx, 1, nullptr, nullptr));
         auto k0 = std::chrono::steady_clock::now();
         CK(run(n_iters));
@@ -140,7 +141,7 @@ int main(int argc, char** argv) {
         const double ks = std::chrono::duration<double>(std::chrono::steady_clock::now() - k0).count();
         CK(avc_ktime(ctx, 0, us, nl));
         printf("{\"ktime_run_ms_per_iter\": %.4f}\n", ks * 1e3 / n_iters);
-        for (int i = 0; i < 16; ++i)
+        for (int i = 0; i < 18; ++i)
             if (nl[i] > 0)
                 printf("{\"ktime_kernel\": \"%s<%s>\", \"launches_per_iter\": %.2f, \"avg_us\": %.3f}\n", kn[i / 2],
                        (i & 1) ? "bf16" : "f32", (double)nl[i] / n_iters, us[i]);

@@ -93,8 +93,10 @@ namespace avc {
 // ---------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------
-template <int PREC, int SH>
-__global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
+// The two passes are device functions: launched on their own (se_fwd_fused / se_bwd_fused) or back to back per
+// iteration inside the persistent attack kernel (se_attack_fused, KT = false: no per-pass kernel stamps).
+template <int PREC, int SH, bool KT>
+__device__ __forceinline__ void se_fwd_body(const FusedArgs& A) {
     constexpr int STD = (SH == 0 || SH == 16) ? 1 : 0;
     constexpr bool RT = SH == 16;               // standard classes, runtime frame counts
     constexpr int G = STD ? 8 : SH;             // fragments per (non-dgrad) layer
@@ -106,20 +108,25 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
     constexpr bool DBUF = PREC == PREC_BF16;   // double-buffered bank output (LDS room)
     // bf16, standard shape (ReLU, no ContentEncoder InstanceNorm there): bank / conv1 epilogues pack first
     constexpr bool PKRELU = AVC_FZ_PKRELU && PREC == PREC_BF16 && STD != 0;
-    const int b = blockIdx.x;
+    int b = blockIdx.x;
+    if constexpr (!KT) asm volatile("" : "+s"(b));   // (persistent kernel: nothing derived from it crosses a pass)
     const int T = (STD && !RT) ? StdSE::T : A.T;
     const int nb = STD ? StdSE::NB : A.nb;
     const int nblk = STD ? StdSE::NBLK : A.nblk;
     const int ks = STD ? StdSE::KSZ : A.ks;
     const int P = ks / 2;
-    const int tid = threadIdx.x, lane = tid & 63;
+    int tid = threadIdx.x;
+    // (persistent kernel: the lane index made opaque per pass, so LICM cannot hoist the lane-derived LDS / HBM
+    // offsets of both passes out of the iteration loop -- live across it they spilled ~1k VGPRs)
+    if constexpr (!KT) asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
     const int act = STD ? 0 : A.act;                   // the standard shape is ReLU (host-checked)
     FZ_PH_DECL
     FZ_PH();
     KTime* const kt = &g_ktime_fused[KT_FUSED_FWD + (PREC == PREC_BF16)];
-    const KtStart kts = ktime_begin(kt);
+    const KtStart kts = KT ? ktime_begin(kt) : KtStart{0ull, false};
     if (A.tick && b == 0 && tid == 0) atomicAdd(A.tick, 1);
 
     char* XB = fz_lds;                                  // x image [T+8][80], pad 4
@@ -511,8 +518,9 @@ __global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
 // ---------------------------------------------------------------------------------
 // backward + Adam
 // ---------------------------------------------------------------------------------
-template <int PREC, int SH>
-__global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
+// sraw: the Adam step counter as the iteration sees it (1-based; the loss-history row and the grad0 test)
+template <int PREC, int SH, bool KT>
+__device__ __forceinline__ void se_bwd_body(const FusedArgs& A, const int sraw) {
     constexpr int STD = (SH == 0 || SH == 16) ? 1 : 0;
     constexpr bool RT = SH == 16;               // standard classes, runtime frame counts
     // the 128-frame LDS layout with unconditional stores (bf16; the fp32 instance of it crashes the gfx950
@@ -528,12 +536,17 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     constexpr int ZPB = 8;         // ... around a bank dY image
     constexpr int EB = 4;          // bank dgrad edge columns per side
     constexpr int WPL = FZ_MASK_WORDS_PER_LAYER / 4;
-    const int b = blockIdx.x;
+    int b = blockIdx.x;
+    if constexpr (!KT) asm volatile("" : "+s"(b));   // (persistent kernel: nothing derived from it crosses a pass)
     const int T = (STD && !RT) ? StdSE::T : A.T;
     const int nb = STD ? StdSE::NB : A.nb;
     const int ks = STD ? StdSE::KSZ : A.ks;
     const int P = ks / 2;
-    const int tid = threadIdx.x, lane = tid & 63;
+    int tid = threadIdx.x;
+    // (persistent kernel: the lane index made opaque per pass, so LICM cannot hoist the lane-derived LDS / HBM
+    // offsets of both passes out of the iteration loop -- live across it they spilled ~1k VGPRs)
+    if constexpr (!KT) asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, kq = lane >> 4;
     const int act = STD ? 0 : A.act;                   // the standard shape is ReLU (host-checked)
@@ -541,7 +554,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     FZ_PH_DECL
     FZ_PH();
     KTime* const kt = &g_ktime_fused[KT_FUSED_BWD + (PREC == PREC_BF16)];
-    const KtStart kts = ktime_begin(kt);
+    const KtStart kts = KT ? ktime_begin(kt) : KtStart{0ull, false};
     const u64* mbase = A.masks + (size_t)b * A.mask_words;
     // Shape-generic bf16 kernels read the ReLU' words from an LDS copy of the utterance's set (made once,
     // below): their K loops have runtime step counts, so the waitcnt pass cannot count the weight-ring loads
@@ -895,7 +908,7 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     FZ_PH();
 
     if (A.gx_out && A.losses && tid == 0) {   // fb: the fused head's loss of SE(dec) -> history row
-        const int sn = *A.step;
+        const int sn = sraw;
         if (sn >= 1 && sn <= A.loss_len) A.losses[(size_t)(sn - 1) * A.B + b] = A.loss_cur[b];
     }
     // RT: item k of a thread is (row ci, frames 4g .. 4g+3) of the padded [80][132] rows, g < 32; its frames
@@ -952,10 +965,10 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     const AdamArgs& Ad = A.adam;
     const float eps = A.scal[0];
     if (A.losses && tid == 0) {   // the fused head's loss of this iteration -> history row step-1
-        const int sn = *A.step;
+        const int sn = sraw;
         if (sn >= 1 && sn <= A.loss_len) A.losses[(size_t)(sn - 1) * A.B + b] = A.loss_cur[b];
     }
-    const int step = min(max(*A.step, 1), A.table_len);
+    const int step = min(max(sraw, 1), A.table_len);
     const float nstep = Ad.table[2 * (step - 1)];
     const float bc2s = Ad.table[2 * (step - 1) + 1];
     const float rbc2s = 1.f / bc2s;
@@ -1051,6 +1064,59 @@ __global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
     ktime_end(kt, kts);
 }
 
+template <int PREC, int SH>
+__global__ void __launch_bounds__(256, 1) se_fwd_fused(FusedArgs A) {
+    se_fwd_body<PREC, SH, true>(A);
+}
+template <int PREC, int SH>
+__global__ void __launch_bounds__(256, 1) se_bwd_fused(FusedArgs A) {
+    se_bwd_body<PREC, SH, true>(A, *A.step);
+}
+
+// ---------------------------------------------------------------------------------
+// Persistent emb attack: n_iters iterations (forward + fused head + backward + Adam) of ONE utterance per
+// workgroup in one launch.  The utterances share nothing inside an iteration (per-utterance loss, gradient
+// and Adam state), so a workgroup runs its utterance's iterations back to back: no kernel boundary per pass
+// (where every workgroup waited for the slowest one and the next launch's ramp-up) -- the separate launches
+// spent ~5 us per emb iteration between kernels.  Everything a pass hands to the next (adv, ReLU' words,
+// pooled / g_pooled, the loss) is this workgroup's own and goes through its CU's write-through L1, so a
+// workgroup-scope fence and barrier order it.  The step counter is read once (every workgroup, at its start)
+// and advanced by fz_step_add after the launch, so the launch never races its own reads of it.
+// ---------------------------------------------------------------------------------
+template <int PREC, int SH>
+__global__ void __launch_bounds__(256, 1) se_attack_fused(AtkArgs A) {
+    // (the launch's start stamp parked in LDS and the loop bound re-read per iteration: the bodies run at the
+    // scalar register limit, and every SGPR live across the loop spilled into VGPR lanes inside them)
+    __shared__ unsigned long long kt_t0, kt_on;
+    {
+        const KtStart k0 = ktime_begin(&g_ktime_fused[KT_FUSED_ATK + (PREC == PREC_BF16)]);
+        if (threadIdx.x == 0) {
+            kt_t0 = k0.t0;
+            kt_on = k0.on ? 1ull : 0ull;
+        }
+    }
+    const int s0 = *A.b.step;
+    // the arguments read through the kernarg pointer made opaque per iteration: no field load (or address
+    // derived from one) is loop-invariant, so none is hoisted and kept live across the loop (taking the
+    // parameter's address instead would make a private copy of it)
+    for (int st = s0 + 1;; ++st) {
+        auto kp = __builtin_amdgcn_kernarg_segment_ptr();   // (constant address space: scalar loads)
+        asm volatile("" : "+s"(kp));
+        const AtkArgs* ap = (const AtkArgs*)kp;
+        if (st > s0 + ap->n_iters) break;
+        se_fwd_body<PREC, SH, false>(ap->f);
+        __threadfence_block();
+        __syncthreads();
+        se_bwd_body<PREC, SH, false>(ap->b, st);
+        __threadfence_block();
+        __syncthreads();
+    }
+    ktime_end(&g_ktime_fused[KT_FUSED_ATK + (PREC == PREC_BF16)], KtStart{kt_t0, kt_on != 0ull});
+}
+__global__ void fz_step_add(int32_t* step, int n) {
+    if (threadIdx.x == 0) step[0] += n;
+}
+
 #define AVC_FZ_INST(P, S)                                        \
     template __global__ void se_fwd_fused<P, S>(FusedArgs);     \
     template __global__ void se_bwd_fused<P, S>(FusedArgs);
@@ -1066,6 +1132,7 @@ AVC_FZ_INST(PREC_BF16, 2)
 AVC_FZ_INST(PREC_BF16, 4)
 AVC_FZ_INST(PREC_BF16, 8)
 AVC_FZ_INST(PREC_BF16, 16)
+template __global__ void se_attack_fused<PREC_BF16, 0>(AtkArgs);
 #undef AVC_FZ_INST
 
 }  // namespace avc

@@ -188,6 +188,12 @@ struct FusedArgs {
                                       // T frames at b * 80 * T)
 };
 
+// persistent emb attack (se_attack_fused): the forward's and the backward's arguments and the iteration count
+struct AtkArgs {
+    FusedArgs f, b;
+    int32_t n_iters;
+};
+
 // ---------------------------------------------------------------------------------
 // Long-utterance engine (avc_long.hip): any T (the fused engine's LDS images stop at 128
 // frames).  Still one workgroup of 4 waves per utterance and wave w owns channels

@@ -23,7 +23,7 @@ struct KTime {
     unsigned long long pad[2];
 };
 constexpr int KT_SLOTS = 8;       // records per translation unit: kernel k at 2k (fp32) and 2k + 1 (bf16)
-constexpr int KT_FUSED_FWD = 0, KT_FUSED_BWD = 2;                              // avc_fused.hip
+constexpr int KT_FUSED_FWD = 0, KT_FUSED_BWD = 2, KT_FUSED_ATK = 4;           // avc_fused.hip
 constexpr int KT_LZ_SE_FWD = 0, KT_LZ_SE_BWD = 2, KT_LZ_DEC_FWD = 4, KT_LZ_DEC_BWD = 6;   // avc_long.hip
 constexpr int KT_DEC_FWD = 0, KT_DEC_BWD = 2;                                  // avc_vc.hip
 

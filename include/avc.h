@@ -390,8 +390,9 @@ int avc_profile_kernel(avc_ctx* ctx, int i, char* name, int name_len, long* laun
  * start and end; a launch spans the earliest start to the latest end).  enable = 1 resets and starts
  * recording (process-wide, on ctx's device); enable = 0 stops and writes, per kernel and precision in
  * the order se_fwd_fused, se_bwd_fused, lz_se_fwd, lz_se_bwd, lz_dec_fwd, lz_dec_bwd, dec_fwd_fused,
- * dec_bwd_fused, each as <fp32> then <bf16>, the average launch duration in microseconds into avg_us[16]
- * and the launch count into launches[16] (either may be NULL).  Synchronises ctx's stream. */
+ * dec_bwd_fused, se_attack_fused (the persistent emb attack: one launch per call), each as <fp32> then
+ * <bf16>, the average launch duration in microseconds into avg_us[18] and the launch count into
+ * launches[18] (either may be NULL).  Synchronises the device. */
 int avc_ktime(avc_ctx* ctx, int enable, double* avg_us, int64_t* launches);
 
 /* Workspace cache of a context.  A context keeps the buffers, launch plans and captured hipGraphs

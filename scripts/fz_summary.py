@@ -96,6 +96,9 @@ def main():
     ap.add_argument("--pmc-json", default=None, help="merge per-kernel traffic / mfma_util into this file "
                                                       "under --key (read by bench.py)")
     ap.add_argument("--key", default=None, help="e.g. emb, emb_fp32, e2e, fb")
+    ap.add_argument("--iters-per-launch", type=int, default=None,
+                    help="attack iterations per dispatch of the persistent kernel (se_attack_fused): recorded "
+                         "with its row so bench.py reports its traffic per iteration")
     a = ap.parse_args()
     src = src_hash(a.dir)
     per = load_counters(a.dir, a.warm)
@@ -146,7 +149,10 @@ def main():
                      f"avc_bench; first {a.warm} dispatches per kernel skipped).  MFMA util = "
                      "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x min(GRBM_GUI_ACTIVE/8, trace duration x 2.4 GHz)); * = the "
                      "counter window outlasted the dispatch, cycles taken from the trace duration.  HBM = 2 x FETCH_SIZE + "
-                     "WRITE_SIZE.  Wave state = fractions of SQ_WAVE_CYCLES.\n\n" + txt + "\n")
+                     "WRITE_SIZE.  Wave state = fractions of SQ_WAVE_CYCLES." +
+                     (f"  `se_attack_fused` (the persistent emb attack) runs {a.iters_per_launch} iterations per "
+                      "dispatch: divide its duration and HBM bytes by that for one iteration."
+                      if a.iters_per_launch else "") + "\n\n" + txt + "\n")
         json.dump(out_json, open(a.out + "_counters.json", "w"), indent=1)
         st = glob.glob(os.path.join(a.dir, "trace", "**", "*kernel_stats.csv"), recursive=True)
         if st:
@@ -154,7 +160,10 @@ def main():
     if a.pmc_json and a.key:
         db = json.load(open(a.pmc_json)) if os.path.exists(a.pmc_json) else {}
         db[a.key] = {libname(k): {"traffic": d["hbm_bytes"], "mfma_util": d["mfma_util"], "median_us": d["median_us"],
-                                  "source": (a.out or a.dir) + "_summary.md", "src": src} for k, d in rows}
+                                  "source": (a.out or a.dir) + "_summary.md", "src": src,
+                                  **({"iters_per_launch": a.iters_per_launch}
+                                     if a.iters_per_launch and k.startswith("se_attack_fused") else {})}
+                     for k, d in rows}
         json.dump(db, open(a.pmc_json, "w"), indent=1, sort_keys=True)
 
 

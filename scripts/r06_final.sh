@@ -17,7 +17,7 @@ run() {   # name timeout args...
 }
 case "${STAGE:-A}" in
 A)
-  IFS=';' read -ra CFGS <<< "${PMC_CFGS:-1 0 128 20;1 1 128 10;1 2 128 10;1 0 400 10;1 1 400 6;1 2 400 6}"
+  IFS=';' read -ra CFGS <<< "${PMC_CFGS:-1 0 128 10;1 1 128 6;1 2 128 6;1 0 400 4;1 1 400 3;1 2 400 3}"
   for cfg in "${CFGS[@]}"; do
     set -- $cfg
     PREC=$1 ATTACK=$2 T=$3 ITERS=$4 bash scripts/pmc_fused.sh > gpurun_out/pmc_${1}_${2}_${3}.log 2>&1
