@@ -499,6 +499,7 @@ static int set_fused_attrs() {
     const int atk = std::max(std::max(fz_lds_fwd(PREC_BF16, 128, 5), (int)((4 * 6 + 8) * FZ_C * sizeof(float))),
                              fz_lds_bwd_launch(PREC_BF16, 128, 16, 25 * FZ_MASK_WORDS_PER_LAYER));
     HIPCHK(hipFuncSetAttribute((const void*)se_attack_fused<PREC_BF16, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, atk));
+    HIPCHK(hipFuncSetAttribute((const void*)se_attack_fused<PREC_BF16, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, atk));
     for (const void* fn : {(const void*)lz_se_fwd<PREC_F32>, (const void*)lz_se_fwd<PREC_BF16>,
                            (const void*)lz_se_bwd<PREC_F32>, (const void*)lz_se_bwd<PREC_BF16>,
                            (const void*)lz_dec_fwd<PREC_F32>, (const void*)lz_dec_fwd<PREC_BF16>,
@@ -1993,11 +1994,13 @@ static int stage_call_consts(avc_ctx* ctx, int n_iters, const float scal[4], dou
 static bool persist_ok(const Plan& iter) {
     const char* e = getenv("AVC_PERSIST");   // (read per call: tests compare both paths in one process)
     const bool off = e && e[0] == '0';
+    const char* e16 = getenv("AVC_PERSIST16");   // A/B: the runtime-length shape on per-pass launches
+    const bool persist16_off = e16 && e16[0] == '0';
     if (off || iter.launches.size() != 2) return false;
     const Launch& F = iter.launches[0];
     const Launch& Bk = iter.launches[1];
     return F.kind == L_FZ_FWD && Bk.kind == L_FZ_BWD && F.prec == PREC_BF16 && Bk.prec == PREC_BF16 &&
-           F.fz.fuse_head == 1 && F.fz_shape == Bk.fz_shape && F.fz_shape == 0 &&
+           F.fz.fuse_head == 1 && F.fz_shape == Bk.fz_shape && (F.fz_shape == 0 || (F.fz_shape == 16 && !persist16_off)) &&
            !Bk.fz.gx_out && Bk.fz.fuse_head == 0 && F.fz.tick == Bk.fz.step;
 }
 static int run_persist(avc_ctx* ctx, const Plan& iter, int n_iters) {
@@ -2010,7 +2013,8 @@ static int run_persist(avc_ctx* ctx, const Plan& iter, int n_iters) {
     a.b = Bk.fz;
     a.n_iters = n_iters;
     const size_t sh = std::max(F.shmem, Bk.shmem);
-    hipLaunchKernelGGL((se_attack_fused<PREC_BF16, 0>), F.grid, F.block, sh, ctx->stream, a);
+    if (F.fz_shape == 0) hipLaunchKernelGGL((se_attack_fused<PREC_BF16, 0>), F.grid, F.block, sh, ctx->stream, a);
+    else hipLaunchKernelGGL((se_attack_fused<PREC_BF16, 16>), F.grid, F.block, sh, ctx->stream, a);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(fz_step_add, dim3(1), dim3(64), 0, ctx->stream, F.fz.tick, n_iters);
     HIPCHK(hipGetLastError());

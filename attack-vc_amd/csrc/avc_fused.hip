@@ -1133,6 +1133,7 @@ AVC_FZ_INST(PREC_BF16, 4)
 AVC_FZ_INST(PREC_BF16, 8)
 AVC_FZ_INST(PREC_BF16, 16)
 template __global__ void se_attack_fused<PREC_BF16, 0>(AtkArgs);
+template __global__ void se_attack_fused<PREC_BF16, 16>(AtkArgs);
 #undef AVC_FZ_INST
 
 }  // namespace avc

@@ -29,10 +29,11 @@ def _ctx(m):
                               DEV.index or 0)
 
 
-@pytest.mark.parametrize("B,n", [(6, 55), (5, 1), (300, 3)])
-def test_persistent_equals_per_pass(full, B, n, monkeypatch):
-    g = torch.Generator().manual_seed(9300 + B + n)
-    vc, at, p0 = (torch.randn(B, 80, 128, generator=g).to(DEV) for _ in range(3))
+@pytest.mark.parametrize("B,n,T", [(6, 55, 128), (5, 1, 128), (300, 3, 128), (6, 55, 120), (4, 7, 97)])
+def test_persistent_equals_per_pass(full, B, n, T, monkeypatch):
+    """T = 128: the standard kernels; T = 120 / 97: the runtime-length ones (shape 16)."""
+    g = torch.Generator().manual_seed(9300 + B + n + T)
+    vc, at, p0 = (torch.randn(B, 80, T, generator=g).to(DEV) for _ in range(3))
     a = _ctx(full)
     a.ktime_start()
     r1 = a.emb_attack(vc, at, p0, 0.1, n, precision="bf16", want_losses=True, want_grad0=True)
