@@ -47,7 +47,11 @@ def main():
                 for c, v in cs.items():
                     ctr[name[d]][c].append(v)
     traffic = {}
-    lines = ["# rocprofv3 summary r01: mel2wav back end (B=256 mels 80x128, 100 Griffin-Lim iterations)", "",
+    import re
+    tl = a.dir.rstrip("/") + ".trace.log"
+    m = re.search(r"src=([0-9a-f]{16})", open(tl).read()) if os.path.exists(tl) else None
+    lines = [f"# rocprofv3 summary {a.round}: mel2wav back end (B=256 mels 80x128, 100 Griffin-Lim iterations)", "",
+             f"libavc src={m.group(1) if m else 'unknown'}.", "",
              "Source: `scripts/pmc_dsp.sh` on one MI355X: `python3 bench.py --attack mel2wav --steps 1 --warmup 0` under "
              "`rocprofv3 --kernel-trace --stats`, plus one run per PMC pass.  HBM = 2*FETCH_SIZE + WRITE_SIZE.", "",
              "| kernel | launches | median us | HBM MB/launch | HBM GB/s | LDS insts/launch | LDS bank confl / LDS active |",
