@@ -559,6 +559,16 @@ def main_lengths(a):
     def step(prec=a.precision, n=a.n_iters):
         return batching.attack_many("emb", [model_dev], vc, at, a.eps, n, ptb0s=p0, precision=prec, max_batch=B,
                                     ragged=not a.bucketed)
+    # heartbeat on stderr: a per-length-bucket step (hundreds of single-utterance buckets) runs minutes
+    # without output
+    import threading
+    hb_stop = threading.Event()
+
+    def heartbeat():
+        t_hb = time.perf_counter()
+        while not hb_stop.wait(30.0):
+            print(f"bench --lengths: running ({time.perf_counter() - t_hb:.0f} s)", file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -573,6 +583,7 @@ def main_lengths(a):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, None)
+    hb_stop.set()
     assert all(torch.isfinite(o).all() for o in out)
     frames = sum(lens_all)
     roof = None
