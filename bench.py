@@ -738,13 +738,15 @@ def main():
         else:
             ctx = avc_native.vc_context_for(model_dev, dev)
         # the hot kernels' durations INSIDE the captured graph replay, no profiler attached: device
-        # wall-clock stamps per workgroup (avc_ktime), over KTIME_ITERS graph-replayed iterations right
-        # after the timed region (same workspace, same graphs)
+        # wall-clock stamps per workgroup (avc_ktime), over one more attack of the timed step's n_iters (the
+        # persistent emb kernel's launch span depends on its length: clock ramp-up is amortised over it)
+        # (right after the timed region: same workspace, same graphs)
+        kti = a.n_iters
         ctx.ktime_start()
         if a.attack == "emb":
-            ctx.emb_attack(vc, at, p0, a.eps, KTIME_ITERS, precision=a.precision)
+            ctx.emb_attack(vc, at, p0, a.eps, kti, precision=a.precision)
         else:
-            ctx.vc_attack(a.attack, src, vc, at, p0, a.eps, KTIME_ITERS, precision=a.precision)
+            ctx.vc_attack(a.attack, src, vc, at, p0, a.eps, kti, precision=a.precision)
         kt = ctx.ktime_stop()
         # per-launch FLOPs and the eager HIP kernel-timestamp durations (each kernel launched alone)
         ctx.set_profiling(True)
@@ -761,23 +763,23 @@ def main():
         atk = "se_attack_fused<bf16>"
         per_iter = None
         if atk in kt:
-            # the persistent emb attack: ONE launch ran all KTIME_ITERS iterations.  Its unit of
+            # the persistent emb attack: ONE launch ran all kti iterations.  Its unit of
             # work is one iteration -- the forward (+ fused head) and backward passes whose FLOPs the per-pass
             # profile below counts -- so achieved = FLOPs per iteration / launch span per iteration
             kn, kus = kt[atk]
             passes = [k for k in ("se_fwd_fused<bf16>", "se_bwd_fused<bf16>") if k in stats]
             fl_it = sum(stats[k][2] for k in passes) / PROF_ITERS
-            per_iter = KTIME_ITERS * kn
+            per_iter = kti * kn
             name, n, tot_fl = atk, 1, fl_it
             tot_ms = sum(stats[k][1] for k in passes) / PROF_ITERS   # the per-pass launches' eager time per iteration
             avg_ms = kus * 1e-3 * kn / per_iter
-            how = (f"in-graph device wall-clock stamps (avc_ktime): {kn} persistent launch(es) of {KTIME_ITERS} "
+            how = (f"in-graph device wall-clock stamps (avc_ktime): {kn} persistent launch(es) of {kti} "
                    f"iterations, per iteration")
         elif timed:   # dominant kernel by in-graph time per iteration
             base, (kn, kus) = max(timed.items(), key=lambda kv: kv[1][0] * kv[1][1])
             name, (n, tot_ms, tot_fl) = eager[base]
             avg_ms = kus * 1e-3
-            how = f"in-graph device wall-clock stamps (avc_ktime), {kn} launches over {KTIME_ITERS} iterations"
+            how = f"in-graph device wall-clock stamps (avc_ktime), {kn} launches over {kti} iterations"
         else:       # no stamped kernel on this path: the eager per-launch HIP-event timing
             name, (n, tot_ms, tot_fl) = max(stats.items(), key=lambda kv: kv[1][1])
             avg_ms = tot_ms / n
@@ -790,13 +792,13 @@ def main():
                 "avg_launch_ms_eager": round(e_ms, 5),
                 "frac_eager": round((tot_fl / n) / (e_ms * 1e-3) / 1e12 / peak, 4),
                 "iter_ms_profiled": round(ms_iter, 4),
-                "in_graph": {k: {"launches_per_iter": v[0] / KTIME_ITERS, "avg_ms": round(v[1] * 1e-3, 5),
+                "in_graph": {k: {"launches_per_iter": v[0] / kti, "avg_ms": round(v[1] * 1e-3, 5),
                                  **({"tflops": round(eager[k][1][2] / eager[k][1][0] / (v[1] * 1e-6) / 1e12, 2)}
                                     if k in eager else {})} for k, v in kt.items()},
                 "per_kernel": {k: {"launches_per_iter": v[0] / PROF_ITERS, "avg_ms": round(v[1] / v[0], 4),
                                    "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 2)} for k, v in stats.items()}}
         if per_iter:
-            roof.update(per_iteration=True, avg_launch_ms=round(kus * 1e-3, 4), iters_per_launch=KTIME_ITERS,
+            roof.update(per_iteration=True, avg_launch_ms=round(kus * 1e-3, 4), iters_per_launch=kti,
                         avg_iter_ms=round(avg_ms, 5), flop_per_iteration=tot_fl,
                         avg_launch_ms_eager=None, frac_eager=round(tot_fl / (tot_ms * 1e-3) / 1e12 / peak, 4),
                         iter_ms_eager_passes=round(tot_ms, 5))

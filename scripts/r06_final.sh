@@ -54,5 +54,6 @@ C)
   run bench_lengths_bucketed 600 --lengths 64:600 --bucketed --steps 1 --warmup 1 --no-cpu-baseline
   run bench_lengths_64_128 600 --lengths 64:128 --steps 1 --warmup 1 --no-cpu-baseline
   run bench_lengths_64_128_bucketed 600 --lengths 64:128 --bucketed --steps 1 --warmup 1 --no-cpu-baseline
+  [ -n "${EXTRA:-}" ] && run bench_extra 600 $EXTRA
   echo STAGE_C_OK ;;
 esac
