@@ -51,7 +51,9 @@ C)
     rc=$?; echo "pmc ragged rc=$rc"; tail -1 gpurun_out/pmc_ragged.log; [ $rc -eq 0 ] || exit $rc
   fi
   run bench_lengths 600 --lengths 64:600 --steps 1 --warmup 1
-  run bench_lengths_bucketed 600 --lengths 64:600 --bucketed --steps 1 --warmup 1 --no-cpu-baseline
+  # the per-length-bucket comparison at 64 utterances (one bucket per length: ~1.5 s each on the long engine)
+  run bench_lengths_b64 300 --lengths 64:600 --batch 64 --steps 1 --warmup 1 --no-cpu-baseline
+  run bench_lengths_b64_bucketed 600 --lengths 64:600 --batch 64 --bucketed --steps 1 --warmup 0 --no-cpu-baseline
   run bench_lengths_64_128 600 --lengths 64:128 --steps 1 --warmup 1 --no-cpu-baseline
   run bench_lengths_64_128_bucketed 600 --lengths 64:128 --bucketed --steps 1 --warmup 1 --no-cpu-baseline
   [ -n "${EXTRA:-}" ] && run bench_extra 600 $EXTRA
