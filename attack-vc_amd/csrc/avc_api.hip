@@ -1222,7 +1222,7 @@ static int plan_fused_forward(avc_ctx* ctx, Workspace& ws, Plan& pl, const float
     F.fz.x = x;
     F.fz.write_masks = attack ? 1 : 0;
     F.fz.tick = attack ? ws.step : nullptr;
-    F.fz_shape = fused_shape(ctx, ws.T);
+    F.fz_shape = ws.ragged ? 16 : fused_shape(ctx, ws.T);
     F.flop = ws.flop_fwd;
     F.name = prec == PREC_F32 ? "se_fwd_fused<f32>" : "se_fwd_fused<bf16>";
     if (ws.lz) F.name = prec == PREC_F32 ? "lz_se_fwd<f32>" : "lz_se_fwd<bf16>";
@@ -1292,7 +1292,7 @@ static int plan_fused_backward(avc_ctx* ctx, Workspace& ws, Plan& pl, int prec) 
     L.block = dim3(256);
     L.fz = fused_args(ctx, ws, prec);
     L.lz = ws.lza;
-    L.fz_shape = fused_shape(ctx, ws.T);
+    L.fz_shape = ws.ragged ? 16 : fused_shape(ctx, ws.T);
     // (SH = 16: the LDS images are laid out for the 128-frame bound)
     L.shmem = ws.lz ? LZ_SHMEM : fz_lds_bwd_launch(prec, L.fz_shape == 16 ? 128 : ws.T, L.fz_shape, L.fz.mask_words);
     AdamArgs& A = L.fz.adam;
@@ -1438,11 +1438,18 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters, const std::vector<
     std::vector<std::vector<int>> Tls;
     double flop = 0;
     size_t X = 0;
+    bool rag_fused = false;
     if (lens) {
         if ((int)lens->size() != B) return fail("ragged batch: %zu lengths for B=%d", lens->size(), B);
         if (!ctx->fused_ok || ctx->engine == AVC_ENGINE_LAYERED)
             return fail("ragged batches run on the long engine (fused-capable config, engine not layered)");
         T = *std::max_element(lens->begin(), lens->end());
+        // every length in (64, 128] of the standard config: the fused runtime-length kernels with a
+        // per-workgroup length (LDS images laid out for 128 frames); otherwise the long engine
+        const int Tmin = *std::min_element(lens->begin(), lens->end());
+        const char* rf = getenv("AVC_RAGGED_FUSED");
+        rag_fused = Tmin > 64 && T <= 128 && ctx->engine != AVC_ENGINE_LONG && !(rf && rf[0] == '0') &&
+                    fused_shape(ctx, 100) == 16 && !(getenv("AVC_LONG") && getenv("AVC_LONG")[0] == '1');
         for (int b = 0; b < B; ++b) {
             std::vector<int> t;
             if (enc_block_lengths(ctx, (*lens)[b], t)) return 1;
@@ -1451,12 +1458,13 @@ static int ensure_ws(avc_ctx* ctx, int B, int T, int n_iters, const std::vector<
             Tls.push_back(t);
         }
     }
+    if (rag_fused) T = 128;   // the workspace's bound (LDS layout, mask words); lengths come from ws.rag
     if (enc_block_lengths(ctx, T, Tl)) return 1;
     if (!lens) {
         flop = fz_fwd_flop(c, Tl, ctx->bank_k) * B;
         X = (size_t)B * c.c_in * T;
     }
-    const int eng = lens ? AVC_ENGINE_LONG : engine_for(ctx, T);
+    const int eng = lens ? (rag_fused ? AVC_ENGINE_FUSED : AVC_ENGINE_LONG) : engine_for(ctx, T);
     const bool fused = eng != AVC_ENGINE_LAYERED, lz = eng == AVC_ENGINE_LONG;
     // a cached workspace of this shape (most recently used first)
     auto it = ctx->wss.begin();
@@ -2001,7 +2009,7 @@ static bool persist_ok(const Plan& iter) {
     const Launch& Bk = iter.launches[1];
     return F.kind == L_FZ_FWD && Bk.kind == L_FZ_BWD && F.prec == PREC_BF16 && Bk.prec == PREC_BF16 &&
            F.fz.fuse_head == 1 && F.fz_shape == Bk.fz_shape && (F.fz_shape == 0 || (F.fz_shape == 16 && !persist16_off)) &&
-           !Bk.fz.gx_out && Bk.fz.fuse_head == 0 && F.fz.tick == Bk.fz.step;
+           !Bk.fz.gx_out && Bk.fz.fuse_head == 0 && F.fz.tick == Bk.fz.step && !F.fz.rag;
 }
 static int run_persist(avc_ctx* ctx, const Plan& iter, int n_iters) {
     if (n_iters <= 0) return 0;

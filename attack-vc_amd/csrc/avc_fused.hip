@@ -110,7 +110,12 @@ __device__ __forceinline__ void se_fwd_body(const FusedArgs& A) {
     constexpr bool PKRELU = AVC_FZ_PKRELU && PREC == PREC_BF16 && STD != 0;
     int b = blockIdx.x;
     if constexpr (!KT) asm volatile("" : "+s"(b));   // (persistent kernel: nothing derived from it crosses a pass)
-    const int T = (STD && !RT) ? StdSE::T : A.T;
+    // a ragged batch (runtime-length kernels only): this workgroup's own length and packed offset
+    // (per-pass launches only: with it the persistent shape-16 instance crashed the backend's AGPR-copy pass)
+    const RagUtt* const ru = (RT && KT && A.rag) ? A.rag + b : nullptr;
+    const int T = (STD && !RT) ? StdSE::T : (ru ? ru->T : A.T);
+    const size_t xoff = ru ? (size_t)ru->xoff : (size_t)b * FZ_CIN * T;
+    auto TLr = [&](int l) __attribute__((always_inline)) { return ru ? StdSE::Tl_of(T, l) : A.Tl[l]; };
     const int nb = STD ? StdSE::NB : A.nb;
     const int nblk = STD ? StdSE::NBLK : A.nblk;
     const int ks = STD ? StdSE::KSZ : A.ks;
@@ -170,7 +175,7 @@ __device__ __forceinline__ void se_fwd_body(const FusedArgs& A) {
     const int xt = 32 * w + (lane >> 1), xh = lane & 1;
     float xv[GPT][VE];
     {
-        const float* xs = A.x + (size_t)b * FZ_CIN * T + xt;
+        const float* xs = A.x + xoff + xt;
         if (xt < T) {
 #pragma unroll
             for (int m = 0; m < GPT; ++m)
@@ -440,10 +445,10 @@ __device__ __forceinline__ void se_fwd_body(const FusedArgs& A) {
     if constexpr (STD != 0) {
         static_for<0, StdSE::NBLK>([&](auto L) __attribute__((always_inline)) {
             constexpr int l = decltype(L)::value;
-            block(IC<StdSE::nf(StdSE::Tl(l))>{}, IC<StdSE::nf(StdSE::Tl(l + 1))>{}, l, RT ? A.Tl[l] : StdSE::Tl(l),
-                  RT ? A.Tl[l + 1] : StdSE::Tl(l + 1), StdSE::sub(l));
+            block(IC<StdSE::nf(StdSE::Tl(l))>{}, IC<StdSE::nf(StdSE::Tl(l + 1))>{}, l, RT ? TLr(l) : StdSE::Tl(l),
+                  RT ? TLr(l + 1) : StdSE::Tl(l + 1), StdSE::sub(l));
         });
-        TN = RT ? A.Tl[StdSE::NBLK] : StdSE::Tl(StdSE::NBLK);
+        TN = RT ? TLr(StdSE::NBLK) : StdSE::Tl(StdSE::NBLK);
     } else if (fz_std_sub(A)) {
         // the standard subsample pattern at another length: each block on the fragment count of its
         // own frames (G >> stride-2 blocks before it, at least 1) instead of the input's G -- the deeper
@@ -538,7 +543,12 @@ __device__ __forceinline__ void se_bwd_body(const FusedArgs& A, const int sraw) 
     constexpr int WPL = FZ_MASK_WORDS_PER_LAYER / 4;
     int b = blockIdx.x;
     if constexpr (!KT) asm volatile("" : "+s"(b));   // (persistent kernel: nothing derived from it crosses a pass)
-    const int T = (STD && !RT) ? StdSE::T : A.T;
+    // a ragged batch (runtime-length kernels only): this workgroup's own length and packed offset
+    // (per-pass launches only: with it the persistent shape-16 instance crashed the backend's AGPR-copy pass)
+    const RagUtt* const ru = (RT && KT && A.rag) ? A.rag + b : nullptr;
+    const int T = (STD && !RT) ? StdSE::T : (ru ? ru->T : A.T);
+    const size_t xoff = ru ? (size_t)ru->xoff : (size_t)b * FZ_CIN * T;
+    auto TLr = [&](int l) __attribute__((always_inline)) { return ru ? StdSE::Tl_of(T, l) : A.Tl[l]; };
     const int nb = STD ? StdSE::NB : A.nb;
     const int ks = STD ? StdSE::KSZ : A.ks;
     const int P = ks / 2;
@@ -569,7 +579,7 @@ __device__ __forceinline__ void se_bwd_body(const FusedArgs& A, const int sraw) 
 
     // g_pooled, then the first GEMM's weight ring and mask words, are issued before the
     // LDS clearing so their latency hides under it
-    const int TN = (STD && !RT) ? StdSE::Tl(StdSE::NBLK) : A.Tl[A.nblk];
+    const int TN = (STD && !RT) ? StdSE::Tl(StdSE::NBLK) : (RT ? TLr(StdSE::NBLK) : A.Tl[A.nblk]);
     f32x4 gp[2];
     if constexpr (PREC == PREC_BF16 && STD != 0) {
         if (A.fuse_head == 3) {   // e2e / fb: the head's backward (se_head_v mode 3) runs here
@@ -746,8 +756,8 @@ __device__ __forceinline__ void se_bwd_body(const FusedArgs& A, const int sraw) 
         static_for<0, StdSE::NBLK>([&](auto L) __attribute__((always_inline)) {
             constexpr int l = StdSE::NBLK - 1 - decltype(L)::value;
             constexpr int Tic = StdSE::Tl(l), Toc = StdSE::Tl(l + 1);   // the classes' bounds
-            block(IC<StdSE::nf(Toc)>{}, IC<StdSE::nf(Tic + 2 * (StdSE::KSZ / 2))>{}, l, RT ? A.Tl[l] : Tic,
-                  RT ? A.Tl[l + 1] : Toc, StdSE::sub(l));
+            block(IC<StdSE::nf(Toc)>{}, IC<StdSE::nf(Tic + 2 * (StdSE::KSZ / 2))>{}, l, RT ? TLr(l) : Tic,
+                  RT ? TLr(l + 1) : Toc, StdSE::sub(l));
         });
     } else if (fz_std_sub(A)) {   // per-block fragment counts, as in the forward
         static_for<0, 6>([&](auto L) __attribute__((always_inline)) {
@@ -914,7 +924,7 @@ __device__ __forceinline__ void se_bwd_body(const FusedArgs& A, const int sraw) 
     // RT: item k of a thread is (row ci, frames 4g .. 4g+3) of the padded [80][132] rows, g < 32; its frames
     // t < T are element (ci, t) of the utterance's [80][T] arrays (16-byte accesses when T is a multiple of 4)
     const bool vec4 = (T & 3) == 0;
-    const size_t xbase = (size_t)b * FZ_CIN * T;
+    const size_t xbase = xoff;
     auto rt_item = [&](int k, int& ci, int& g4, int& nok) __attribute__((always_inline)) {
         const int it = tid + 256 * k;          // < 80 * 32 = 2560 = 10 * 256
         ci = it >> 5;
@@ -951,7 +961,7 @@ __device__ __forceinline__ void se_bwd_body(const FusedArgs& A, const int sraw) 
         return;
     }
     if (A.gx_out) {   // d loss / d x handed on (fb: the decoder output's gradient)
-        f32x4* gx = reinterpret_cast<f32x4*>(A.gx_out + (size_t)b * FZ_CIN * T);
+        f32x4* gx = reinterpret_cast<f32x4*>(A.gx_out + xoff);
         const f32x4* R04 = reinterpret_cast<const f32x4*>(R0);
         const f32x4* R14 = reinterpret_cast<const f32x4*>(R1);
         for (int q = tid; q < FZ_CIN * T / 4; q += 256) gx[q] = R04[rq(q)] + R14[rq(q)];
@@ -973,7 +983,7 @@ __device__ __forceinline__ void se_bwd_body(const FusedArgs& A, const int sraw) 
     const float bc2s = Ad.table[2 * (step - 1) + 1];
     const float rbc2s = 1.f / bc2s;
     const AdamStep S{nstep, bc2s, rbc2s, eps, A.scal[3]};
-    const size_t base4 = (size_t)b * FZ_CIN * T / 4;
+    const size_t base4 = xoff / 4;
     f32x4* __restrict__ ptb4 = reinterpret_cast<f32x4*>(Ad.ptb) + base4;
     f32x4* __restrict__ m4 = reinterpret_cast<f32x4*>(Ad.m) + base4;
     f32x4* __restrict__ v4 = reinterpret_cast<f32x4*>(Ad.v) + base4;

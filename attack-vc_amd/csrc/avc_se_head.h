@@ -15,6 +15,12 @@ struct StdSE {
         return t;
     }
     static constexpr int nf(int frames) { return (frames + 15) / 16; }
+    // block l's input length for an utterance of T frames (a ragged batch's per-workgroup length)
+    __host__ __device__ static constexpr int Tl_of(int T, int l) {
+        int t = T;
+        for (int i = 0; i < l; ++i) t = (t + sub(i) - 1) / sub(i);
+        return t;
+    }
 };
 
 

@@ -132,8 +132,10 @@ int avc_emb_attack_emb(avc_ctx* ctx, const float* vc_tgt, const float* tgt_emb, 
  * reflect padding, ceil-mode pooling and time-mean).  vc_tgt, ptb0, out_adv and opts->grad0 are packed
  * [80][lengths[b]] blocks in batch order (device fp32); tgt_emb [B, c_out] = SpeakerEncoder(adv_tgt_b),
  * each adv_tgt embedded at its own length (avc_se_forward).  Every SpeakerEncoder pass is ONE launch over
- * the whole batch (the long engine with per-workgroup lengths and offsets); utterance b's result equals
- * its own avc_emb_attack_emb on the long engine bit for bit.  opts->reduction must be INDEPENDENT.
+ * the whole batch with per-workgroup lengths and offsets: on the fused runtime-length kernels when every
+ * length is in (64, 128] (config.yaml model; env AVC_RAGGED_FUSED=0: never), else on the long engine;
+ * utterance b's result equals its own avc_emb_attack_emb on the same kernels bit for bit.
+ * opts->reduction must be INDEPENDENT.
  * Replaces B calls of attack_utils.emb_attack (attack_utils.py:51-86), one per utterance. */
 int avc_emb_attack_ragged(avc_ctx* ctx, const float* vc_tgt, const int* lengths, int B, const float* tgt_emb,
                           const float* ptb0, float eps, int n_iters, float* out_adv,

@@ -70,6 +70,37 @@ def test_ragged_equals_single_utterance_long(full, prec):
         ctx.set_engine("auto")
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_ragged_fused_runtime_lengths(full, prec, monkeypatch):
+    """Every length in (64, 128]: the ragged batch runs on the fused runtime-length kernels (se_*_fused<*, 16>,
+    per-workgroup length and offset; bf16: the persistent kernel) -- each utterance equals its own attack on the
+    same kernels (AVC_FUSED_RT_FORCE=1 so T = 128 runs them too) bit for bit; AVC_RAGGED_FUSED=0 keeps the long
+    engine, which is checked to be a different path (its timing stamps)."""
+    m, _ = full
+    lens = [128, 127, 120, 113, 100, 97, 80, 65]
+    monkeypatch.setenv("AVC_FUSED_RT_FORCE", "1")
+    ctx = avc_native.Context(avc_native.se_config(m.speaker_encoder), avc_native.flat_weights(m.speaker_encoder),
+                             DEV.index or 0)
+    vc, at, p0 = _utts(lens, 14)
+    te = torch.cat([ctx.se_forward(a[None]) for a in at])
+    ctx.ktime_start()
+    outs, L, g0 = ctx.emb_attack_ragged(vc, te, p0, 0.1, 55, precision=prec, want_losses=True, want_grad0=True)
+    kt = ctx.ktime_stop()
+    assert not any(k.startswith("lz_") for k in kt), kt
+    for b, T in enumerate(lens):
+        ref, Lr, gr = ctx.emb_attack(vc[b][None], None, p0[b][None], 0.1, 55, precision=prec, want_losses=True,
+                                     want_grad0=True, tgt_emb=te[b:b + 1])
+        assert torch.equal(outs[b], ref[0]), (T, float((outs[b] - ref[0]).abs().max()))
+        assert torch.equal(L[:, b], Lr[:, 0]), T
+        assert torch.equal(g0[b], gr[0]), T
+    monkeypatch.setenv("AVC_RAGGED_FUSED", "0")
+    c2 = avc_native.Context(avc_native.se_config(m.speaker_encoder), avc_native.flat_weights(m.speaker_encoder),
+                            DEV.index or 0)
+    c2.ktime_start()
+    c2.emb_attack_ragged(vc, te, p0, 0.1, 3, precision=prec)
+    assert any(k.startswith("lz_se_bwd") for k in c2.ktime_stop())
+
+
 def test_attack_many_ragged(full):
     """attack_many(ragged=True): chunks of any lengths (longest first), results in input order; fp32 equals
     attack_utils.emb_attack per utterance (fused engine for T <= 128, long above) bit for bit."""
