@@ -49,13 +49,16 @@ C)
   if [ "${PMC:-1}" = "1" ]; then
     LO=64 HI=600 bash scripts/pmc_ragged.sh > gpurun_out/pmc_ragged.log 2>&1
     rc=$?; echo "pmc ragged rc=$rc"; tail -1 gpurun_out/pmc_ragged.log; [ $rc -eq 0 ] || exit $rc
+    LO=65 HI=128 bash scripts/pmc_ragged.sh > gpurun_out/pmc_ragged_short.log 2>&1
+    rc=$?; echo "pmc ragged short rc=$rc"; tail -1 gpurun_out/pmc_ragged_short.log; [ $rc -eq 0 ] || exit $rc
   fi
   run bench_lengths 600 --lengths 64:600 --steps 1 --warmup 1
   # the per-length-bucket comparison at 64 utterances (one bucket per length: ~1.5 s each on the long engine)
   run bench_lengths_b64 300 --lengths 64:600 --batch 64 --steps 1 --warmup 1 --no-cpu-baseline
   run bench_lengths_b64_bucketed 600 --lengths 64:600 --batch 64 --bucketed --steps 1 --warmup 0 --no-cpu-baseline
-  run bench_lengths_64_128 600 --lengths 64:128 --steps 1 --warmup 1 --no-cpu-baseline
-  run bench_lengths_64_128_bucketed 600 --lengths 64:128 --bucketed --steps 1 --warmup 1 --no-cpu-baseline
+  # every length in (64, 128]: the ragged batch on the fused runtime-length kernels
+  run bench_lengths_65_128 600 --lengths 65:128 --steps 1 --warmup 1 --no-cpu-baseline
+  run bench_lengths_65_128_bucketed 600 --lengths 65:128 --bucketed --steps 1 --warmup 1 --no-cpu-baseline
   [ -n "${EXTRA:-}" ] && run bench_extra 600 $EXTRA
   echo STAGE_C_OK ;;
 esac
